@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors under tests/golden/ from the REFERENCE ITSELF.
+
+Test infrastructure only.  Runs oracle/_ref/pft_ref (the reference's equation.c/model.c,
+RK_MPI_SAsolver_hybrid2.c and Params front end compiled in place by oracle/Makefile, see
+oracle/ref_harness.c) on modified copies of the reference's default Params
+(apps/intertrack-hybrid-S-freezing/Params) and stores inputs + outputs as compressed npz
+fixtures.  Needs /root/reference and MPICH; the fixtures themselves travel, the reference
+does not.  Re-run with:  make -C oracle ref && python tests/golden/gen_golden.py
+
+Cases (SURVEY.md section 4.2 KATs 1-4):
+  g20      default Params at grid_nodes 20 (10x10x20): parameters, IC (formula + glass
+           beads), RHS at t=0 and after phase_switch_time for calc_mode 0/1/2/10/11,
+           trajectory to several snapshot times (mode 0 and 1; mode 2 with p IC = 0);
+           trajectory also run on 3 ranks and checked byte-identical (F6).
+  ragged   L1=0.036, L2=0.024, grid_nodes 30 -> 18x12x30, random state (seed 20251015),
+           RHS for all modes on 1 and 4 ranks (ranks hold 8/8/7/7 planes), plus every
+           rank's padded input array after bcond_setup+sync_solution (boundary KAT),
+           and single-step solves (accepted and rejected-first).
+"""
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF_APP = "/root/reference/apps/intertrack-hybrid-S-freezing"
+PFT_REF = os.path.join(REPO, "oracle", "_ref", "pft_ref")
+MPIRUN = "/opt/conda/bin/mpirun"
+SEED = 20251015
+ENV = dict(os.environ, OMP_NUM_THREADS="1", OMP_SCHEDULE="static", OMP_PROC_BIND="FALSE")
+
+
+def params_text(replace):
+    src = open(os.path.join(REF_APP, "Params")).read()
+    for key, val in replace.items():
+        if key.startswith("icond "):
+            pat = re.compile(r"^" + re.escape(key) + r"\s*=.*$", re.M)
+            src, n = pat.subn(f'{key} = "{val}"', src)
+        else:
+            pat = re.compile(r"^" + re.escape(key) + r"[ \t]+.*$", re.M)
+            src, n = pat.subn(f"{key}\t{val}", src)
+        assert n == 1, (key, n)
+    return src
+
+
+class Work:
+    def __init__(self, replace):
+        self.dir = tempfile.mkdtemp(prefix="pftgold_")
+        os.symlink(os.path.join(REF_APP, "data"), os.path.join(self.dir, "data"))
+        with open(os.path.join(self.dir, "Params"), "w") as f:
+            f.write(params_text(replace))
+
+    def run(self, nranks, *args, timeout=600):
+        out = os.path.join(self.dir, f"out{nranks}_{abs(hash(args)) % 10**8}")
+        os.makedirs(out, exist_ok=True)
+        cmd = [PFT_REF, args[0], "Params", out] + [str(a) for a in args[1:]]
+        if nranks > 1:
+            cmd = [MPIRUN, "-np", str(nranks)] + cmd
+        subprocess.run(cmd, cwd=self.dir, env=ENV, check=True, timeout=timeout,
+                       stdout=subprocess.DEVNULL)
+        return out
+
+    def close(self):
+        shutil.rmtree(self.dir, ignore_errors=True)
+
+
+def read_params(out):
+    p = {}
+    for line in open(os.path.join(out, "params.txt")):
+        k, v = line.split()
+        p[k] = int(v) if re.fullmatch(r"-?\d+", v) else float.fromhex(v)
+    return p
+
+
+def hexify(p):
+    return {k: (v.hex() if isinstance(v, float) else v) for k, v in p.items()}
+
+
+def load(path, shape):
+    return np.fromfile(path, dtype="<f8").reshape(shape)
+
+
+def random_state(n1, n2, n3, rng):
+    p = rng.uniform(0.0, 1.0, size=(n3, n2, n1))
+    g = rng.uniform(0.0, 1.0, size=(n3, n2, n1))
+    # smooth gl a little so it looks like a phase field, keep it in [0,1]
+    for ax in range(3):
+        g = 0.5 * g + 0.25 * (np.roll(g, 1, ax) + np.roll(g, -1, ax))
+    u = 273.15 + rng.uniform(-20.0, 20.0, size=(n3, n2, n1))
+    return np.stack([u, p, g]).astype("<f8")
+
+
+def traj(out, ncalls, shape):
+    rows = [l.split() for l in open(os.path.join(out, "traj.txt"))]
+    meta = [[float.fromhex(r[0]).hex(), float.fromhex(r[1]).hex(), int(r[2]), int(r[3]), int(r[4])]
+            for r in rows]
+    states = [load(os.path.join(out, f"state{i}.f64"), shape) for i in range(ncalls)]
+    return meta, states
+
+
+def case_g20():
+    arrays, meta = {}, {"case": "g20", "source": "reference Params, grid_nodes 20"}
+    w = Work({"grid_nodes": 20})
+    try:
+        out = w.run(1, "setup")
+        p = read_params(out)
+        n1, n2, n3 = p["n1"], p["n2"], p["n3"]
+        shape = (3, n3, n2, n1)
+        ic = load(os.path.join(out, "ic.f64"), shape)
+        arrays["ic"] = ic
+        meta["params"] = hexify(p)
+        ic_path = os.path.join(w.dir, "ic.f64")
+        ic.tofile(ic_path)
+        # RHS at t = 0 and after the phase switch for every model
+        for mode in (0, 1, 2, 10, 11):
+            wm = Work({"grid_nodes": 20, "calc_mode": mode})
+            try:
+                for tag, t in (("t0", 0.0), ("t1", 20000.0)):
+                    o = wm.run(1, "rhs", ic_path, t)
+                    arrays[f"rhs_m{mode}_{tag}"] = load(os.path.join(o, "rhs.f64"), shape)
+            finally:
+                wm.close()
+        meta["rhs_times"] = {"t0": 0.0, "t1": 20000.0}
+        # trajectories: from IC at t=0, h=tau=1 to several snapshot times (intertrack.c:2272)
+        times = [36.0, 360.0, 720.0]
+        meta["traj_times"] = times
+        for mode, rep in ((0, {}), (1, {}), (2, {"icond p": "0"})):
+            r = {"grid_nodes": 20, "calc_mode": mode}
+            r.update(rep)
+            wm = Work(r)
+            try:
+                o = wm.run(1, "setup")
+                ic_m = load(os.path.join(o, "ic.f64"), shape)
+                icp = os.path.join(wm.dir, "icm.f64")
+                ic_m.tofile(icp)
+                o1 = wm.run(1, "solve", icp, 0.0, 1.0, *times)
+                tm, st = traj(o1, len(times), shape)
+                o3 = wm.run(3, "solve", icp, 0.0, 1.0, *times)
+                tm3, st3 = traj(o3, len(times), shape)
+                assert tm == tm3 and all(np.array_equal(a, b) for a, b in zip(st, st3)), \
+                    f"decomposition invariance broken for mode {mode}"
+                arrays[f"traj_m{mode}_ic"] = ic_m
+                for i, s in enumerate(st):
+                    arrays[f"traj_m{mode}_state{i}"] = s
+                meta[f"traj_m{mode}"] = tm
+            finally:
+                wm.close()
+    finally:
+        w.close()
+    return arrays, meta
+
+
+def case_ragged():
+    arrays, meta = {}, {"case": "ragged", "source": "reference Params, L1=0.036 L2=0.024 grid_nodes 30"}
+    rep = {"L1": 0.036, "L2": 0.024, "grid_nodes": 30}
+    w = Work(rep)
+    try:
+        out = w.run(1, "setup")
+        p = read_params(out)
+        n1, n2, n3 = p["n1"], p["n2"], p["n3"]
+        shape = (3, n3, n2, n1)
+        meta["params"] = hexify(p)
+        st = random_state(n1, n2, n3, np.random.default_rng(SEED))
+        arrays["state"] = st
+        sp = os.path.join(w.dir, "state.f64")
+        st.tofile(sp)
+        for mode in (0, 1, 2, 10, 11):
+            wm = Work(dict(rep, calc_mode=mode))
+            try:
+                for tag, t in (("t0", 100.0), ("t1", 20000.0)):
+                    o1 = wm.run(1, "rhs", sp, t)
+                    o4 = wm.run(4, "rhs", sp, t)
+                    a1 = load(os.path.join(o1, "rhs.f64"), shape)
+                    a4 = load(os.path.join(o4, "rhs.f64"), shape)
+                    assert np.array_equal(a1, a4), f"rhs decomposition mismatch mode {mode}"
+                    arrays[f"rhs_m{mode}_{tag}"] = a1
+                    if mode == 0:
+                        for r in range(4):
+                            arrays[f"w4_{tag}_rank{r}"] = np.fromfile(
+                                os.path.join(o4, f"w_rank{r}.f64"), dtype="<f8")
+                        arrays[f"w1_{tag}_rank0"] = np.fromfile(os.path.join(o1, "w_rank0.f64"), dtype="<f8")
+            finally:
+                wm.close()
+        meta["rhs_times"] = {"t0": 100.0, "t1": 20000.0}
+        # single steps: small h (accepted at once) and a large h (rejected first, then accepted)
+        for tag, (t0, h0, T) in {"small": (100.0, 1e-3, 100.001), "large": (100.0, 5.0, 105.0)}.items():
+            o = w.run(1, "solve", sp, t0, h0, T)
+            tm, sts = traj(o, 1, shape)
+            o4 = w.run(4, "solve", sp, t0, h0, T)
+            tm4, sts4 = traj(o4, 1, shape)
+            assert tm == tm4 and np.array_equal(sts[0], sts4[0])
+            arrays[f"step_{tag}"] = sts[0]
+            meta[f"step_{tag}"] = {"t0": t0, "h0": h0, "T": T, "result": tm[0]}
+    finally:
+        w.close()
+    return arrays, meta
+
+
+def main():
+    if not os.path.exists(PFT_REF):
+        sys.exit("build the reference harness first: make -C oracle ref")
+    for fn in (case_g20, case_ragged):
+        arrays, meta = fn()
+        name = meta["case"]
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrays)
+        with open(os.path.join(HERE, f"{name}.json"), "w") as f:
+            json.dump(meta, f, indent=1, sort_keys=True)
+        print(name, {k: v.shape for k, v in arrays.items()})
+    # the bead centres (data/spheres_positions.txt, data file used by equation.c:35,459-530)
+    beads = np.loadtxt(os.path.join(REF_APP, "data", "spheres_positions.txt"))
+    np.save(os.path.join(HERE, "beads.npy"), beads.astype("<f8"))
+
+
+if __name__ == "__main__":
+    main()
