@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""Benchmark: Mcells x attempted RK-Merson steps per second on MI355X.
+
+One "step" = one attempted Merson step of RK_MPI_SA_solve (the reference's steps_total):
+5 RHS evaluations of the intertrack (u, p, gl) model + 4 stage combines + error norm + the
+update, run by libpft's fused device path with the state resident in HBM.
+
+Workload (N = number of GPUs, one process per GPU, Z-slab decomposition, weak scaling):
+  default Params (apps/intertrack-hybrid-S-freezing/Params, calc_mode 0 GradP) at grid_nodes 400
+  -> 200 x 200 x 400 cells per GPU; with N GPUs the domain is N times taller
+  (200 x 200 x 400N cells, L3 = 0.06 N m), so every GPU holds the 400^3 slab of the 1-GPU case.
+  Initial state: the default Params initial condition (u = 293.15 K, ice cap, glass walls and
+  200 glass beads) built by libpft's host model code; t = 0, h = tau = 1 s.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints one JSON line (contract in the task statement) with `roofline` (dominant stage
+kernel, HIP-event timed) and `cpu_baseline` (the CPU oracle port on a bounded sample, N=1 only).
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+import numpy as np  # noqa: E402
+
+import porousfreezethaw_amd as P  # noqa: E402
+from porousfreezethaw_amd import params as PR  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# algorithmic HBM bytes per cell of each fused stage kernel: doubles read
+# once + written once, perfect stencil reuse.  faithful: u, p, gl all evolved by the solver;
+# gl_static: dgl == 0 exploited (PFT_OPT_GL_STATIC)
+STAGE_DOUBLES = {False: {1: 9, 2: 12, 3: 15, 4: 18, 5: 18}, True: {1: 7, 2: 9, 3: 11, 4: 13, 5: 13}}
+SURVEY_BYTES_PER_CELL_STEP = 840   # unfused solver/RHS boundary accounting
+METRIC = "Mcells·RK-steps/s at 400³ grid, 1/2/4/8 MI355X; % HBM roofline"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--grid-nodes", type=int, default=400, help="grid_nodes of the per-GPU slab")
+    ap.add_argument("--mode", type=int, default=0, help="calc_mode (0 GradP, 1 SigmaP1-P, 2 Temp)")
+    ap.add_argument("--gl-static", action="store_true", help="exploit dgl == 0 (bit-identical)")
+    ap.add_argument("--kz", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--cpu-steps", type=int, default=3, help="attempted steps of the CPU sample")
+    ap.add_argument("--no-timing", action="store_true", help="no HIP-event stage timing")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            sys.exit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+        a.gpus = world
+    L = P.lib()
+    dist = None
+    comm = None
+    if world > 1:
+        # torch.distributed (gloo, host only) is the rendezvous and the barrier; the data path is
+        # libpft's RCCL communicator (pft_comm.h).  torch never touches the GPU here.
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        uid = (C.c_char * 128)()
+        if rank == 0:
+            assert L.pft_comm_get_unique_id(uid) == 0
+        obj = [bytes(uid)]
+        dist.broadcast_object_list(obj, src=0)
+        uid = (C.c_char * 128).from_buffer_copy(obj[0])
+        comm = C.c_void_p()
+        rc = L.pft_comm_init_rccl(C.byref(comm), world, rank, uid, local)
+        if rc:
+            sys.exit(f"rank {rank}: pft_comm_init_rccl failed ({rc})")
+        L.pft_comm_set_current(comm)
+    else:
+        L.pft_hip_set_device(local)
+    L.pft_solver_set_option(P.PFT_OPT_DEVICE, local)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        L.pft_hip_device_sync()
+
+    # ---- workload -------------------------------------------------------------------------
+    base = PR.default_params(grid_nodes=a.grid_nodes, calc_mode=a.mode)
+    n1, n2, n3_slab = base["n1"], base["n2"], base["n3"]
+    total_n3 = n3_slab * world
+    Ls = (base["L1"], base["L2"], base["L3"] * world)
+    prm = P.params_array(base)
+    beads = np.load(os.path.join(REPO, "tests", "golden", "beads.npy"))
+    t0 = time.time()
+    sim = P.Simulation(n1, n2, total_n3, Ls, a.mode, prm, nprocs=world, rank=rank, beads=beads,
+                       tau=base["tau"], tau_min=base["tau_min"], delta=base["delta"],
+                       gl_static=a.gl_static, kz=a.kz or None)
+    init_s = time.time() - t0
+    cells_rank = n1 * n2 * sim.grid.n3
+    cells_total = n1 * n2 * total_n3
+    final_time = base["final_time"]
+
+    # warm-up: uploads x once, builds the kernels' caches; W attempted steps
+    rc = sim.solve_ex(final_time, max(1, a.warmup), P.PFT_SOLVE_KEEP_DEVICE)
+    assert rc == 2, rc
+    st0 = sim.system.steps_total
+    if not a.no_timing:
+        L.pft_solver_set_option(P.PFT_OPT_TIMING, 1)
+    barrier()
+    t1 = time.perf_counter()
+    rc = sim.solve_ex(final_time, a.steps, P.PFT_SOLVE_KEEP_DEVICE | P.PFT_SOLVE_REUSE_DEVICE)
+    barrier()
+    t2 = time.perf_counter()
+    assert rc == 2, rc
+    steps = sim.system.steps_total - st0
+    assert steps == a.steps, (steps, a.steps)
+    el = t2 - t1
+    if dist is not None:
+        import torch
+        tt = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    stats = sim.stats()
+
+    # ---- roofline: dominant fused stage kernel, HIP events on the slab's compute stream -----
+    roof = None
+    if not a.no_timing and stats.stage_n[1] > 0:
+        per = {}
+        for s in range(1, 6):
+            ms = stats.stage_ms[s] / max(1, stats.stage_n[s])
+            byts = STAGE_DOUBLES[a.gl_static][s] * 8 * cells_rank
+            per[s] = (ms, byts)
+        dom = max(per, key=lambda s: per[s][0])
+        ms, byts = per[dom]
+        achieved = byts / (ms * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(REPO, "profiles", "pmc_summary.json")
+        if os.path.exists(pmc):
+            try:
+                ps = json.load(open(pmc))
+                key = f"stage{dom}_gl{int(a.gl_static)}_g{a.grid_nodes}_m{a.mode}"
+                traffic = ps.get(key, {}).get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "kernel": f"merson_stage<{dom},{a.mode},{'true' if a.gl_static else 'false'}>",
+                "algorithmic_bytes_per_launch": byts,
+                "avg_launch_ms": round(ms, 4),
+                "stages_ms": {str(s): round(per[s][0], 4) for s in per},
+                "stages_GBps": {str(s): round(per[s][1] / (per[s][0] * 1e-3) / 1e9, 1) for s in per}}
+
+    value = cells_total * steps / el / 1e6
+    step_bytes = sum(STAGE_DOUBLES[a.gl_static].values()) * 8
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "Mcells·steps/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(el / steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: default Params initial condition (u=293.15 K, ice cap, glass walls, "
+                "200 glass beads from the reference's data file), t=0, h=tau=1",
+        "config": {"workload": f"{a.grid_nodes}^3 default Params per GPU: {n1}x{n2}x{n3_slab} cells/GPU, "
+                               f"global {n1}x{n2}x{total_n3} (Z-slab weak scaling)",
+                   "calc_mode": a.mode, "cells": cells_total, "parallelism": f"zslab{world}",
+                   "gl_static": a.gl_static, "kz": a.kz or 16,
+                   "accepted_steps_total": int(sim.system.steps), "t_end": sim.t},
+        "roofline": roof,
+        "fused_effective_GBps": round(step_bytes * cells_total * steps / el / 1e9 / world, 1),
+        "survey_840B_equiv_GBps": round(SURVEY_BYTES_PER_CELL_STEP * cells_total * steps / el / 1e9 / world, 1),
+        "init_s": round(init_s, 2),
+    }
+
+    # ---- CPU baseline (rank 0, N = 1 only): the oracle port, bounded sample -----------------
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu:
+        cpu = cpu_baseline(sim, base, a)
+    out["cpu_baseline"] = cpu
+    sim.close()
+    if comm is not None:
+        L.pft_comm_set_current(None)
+        L.pft_comm_destroy(comm)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(sim, base, a):
+    """Time the CPU restatement of the reference (oracle/pft_oracle.c: plain C, OpenMP over
+    z-planes, the reference's arithmetic) on the same 400^3 state for a few attempted steps."""
+    try:
+        import _oracle as O
+    except Exception as e:  # noqa: BLE001
+        return {"error": f"oracle unavailable: {e}"}
+    if not os.path.exists(O.LIB_PATH):
+        return {"error": "oracle not built"}
+    g = sim.grid
+    info = {"n1": g.n1, "n2": g.n2, "n3": g.total_n3, "L1": g.L1, "L2": g.L2, "L3": g.L3}
+    sim.download()
+    x0 = sim.interior()
+    prm = P.params_array(base)
+    og = O.make_grid(info)
+    xp = O.pad(og, x0)
+    t, h = C.c_double(sim.t), C.c_double(sim.h)
+    s, stt = C.c_long(0), C.c_long(0)
+    t0 = time.perf_counter()
+    O.lib().pft_or_solve(C.byref(og), O.ptr(prm), a.mode, base["final_time"], C.byref(t), C.byref(h),
+                         base["tau_min"], base["delta"], 0, O.ptr(xp), C.byref(s), C.byref(stt),
+                         a.cpu_steps, O.EXCHANGE_FN(), O.ALLREDUCE_FN(), None)
+    el = time.perf_counter() - t0
+    cores = int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count() or 1)))
+    cells = g.n1 * g.n2 * g.total_n3
+    return {"value": round(cells * stt.value / el / 1e6, 3), "unit": "Mcells·steps/s", "cores": cores,
+            "kind": "port",
+            "sample": f"{stt.value} attempted steps of the same {g.n1}x{g.n2}x{g.total_n3} state, "
+                      f"oracle/pft_oracle.c (gcc -O2, OpenMP {cores} threads), {el:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

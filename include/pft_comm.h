@@ -1,0 +1,69 @@
+/*
+ * pft_comm.h -- the inter-slab communicator that replaces the reference's MPI traffic on the
+ * hot path (SURVEY.md section 2 "Every MPI call site"):
+ *   - sync_solution (equation.c:290-326, MPI_Isend/Irecv/Waitall of 2 ghost planes x 3 vars)
+ *       -> pft_comm_halo: ONE ghost plane per field and direction (the 7-point stencil reads only
+ *          the first ghost layer), RCCL grouped ncclSend/ncclRecv over xGMI on a dedicated HIP
+ *          stream, overlapped with the interior sweep;
+ *   - MPI_Allreduce(MAX) of eps (hybrid2.c:572) -> pft_comm_allreduce_eps (device buffer, RCCL);
+ *   - MPI_Bcast of t/h/delta/... and of the command (hybrid2.c:328-336,616,690) -> pft_comm_bcast.
+ *
+ * One process per GPU: rank r drives GPU `device` and holds Z-slab r (rank 0 = bottom).
+ * Transports: "self" (1 rank), "rccl" (one process per GPU, production), "loopback" (several
+ * slabs in ONE process, one host thread per slab, device-to-device copies; used to exercise
+ * the multi-slab path on a single GPU).  The communicator in use is per host thread
+ * (pft_comm_set_current), as the reference solver's MPI state is per process.
+ */
+#ifndef PFT_COMM_H
+#define PFT_COMM_H
+
+#include "pft_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pft_comm pft_comm;
+
+#define PFT_UNIQUE_ID_BYTES 128
+
+int pft_comm_init_self(pft_comm ** c);
+/* rank 0 creates the id, every rank passes the same bytes (exchange them out of band, e.g.
+   through torch.distributed's store) */
+int pft_comm_get_unique_id(void * id_bytes);
+int pft_comm_init_rccl(pft_comm ** c, int nranks, int rank, const void * id_bytes, int device);
+/* loopback: create once, then each of the nranks threads calls pft_comm_loopback_rank() */
+int pft_comm_init_loopback(pft_comm ** group, int nranks);
+int pft_comm_loopback_rank(pft_comm * group, int rank, pft_comm ** mine);
+int pft_comm_destroy(pft_comm * c);
+
+int pft_comm_rank(const pft_comm * c);
+int pft_comm_size(const pft_comm * c);
+const char * pft_comm_kind(const pft_comm * c);
+
+/* per-thread current communicator (RK_MPI_SA_init binds to it; NULL = self) */
+int pft_comm_set_current(pft_comm * c);
+pft_comm * pft_comm_current(void);
+
+/* attach the slab whose buffers are exchanged */
+int pft_comm_attach(pft_comm * c, pft_slab * s);
+
+/* exchange the boundary planes of buffer `buf` (fields [f0, f1)) with the z-neighbours.
+   halo_start: ordered after the work already on the slab's compute stream, runs on the slab's
+   communication stream, so kernels enqueued on the compute stream afterwards (the interior
+   sweep) overlap it; halo_finish: the compute stream waits for the exchange.
+   No-ops for a single rank. */
+int pft_comm_halo_start(pft_comm * c, int buf, int f0, int f1);
+int pft_comm_halo_finish(pft_comm * c);
+int pft_comm_halo(pft_comm * c, int buf, int f0, int f1);   /* start + finish */
+/* eps max over ranks, on the slab's scratch (u64 bits + non-finite flag), stream-ordered */
+int pft_comm_allreduce_eps(pft_comm * c);
+/* host-level collectives used outside the per-stage path */
+int pft_comm_bcast(pft_comm * c, void * data, int bytes, int root);
+int pft_comm_allreduce_max_i64(pft_comm * c, long long * v);
+int pft_comm_barrier(pft_comm * c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,136 @@
+/*
+ * pft_hip.h -- the thin C-ABI shim between libpft's host C code (rk_solver.c, model.c) and
+ * the hand-written HIP kernels for gfx950 (porousfreezethaw_amd/csrc/pft_kernels.hip).
+ *
+ * Conventions: extern "C"; every call returns int (0 = OK, negative = HIP error, mirroring the
+ * reference's negative codes); streams are explicit (opaque handles); no exceptions cross the
+ * ABI; device buffers are owned by a pft_slab object.  No torch types anywhere.
+ *
+ * Device layout of one slab (one Z-slab of the reference decomposition, intertrack.c:1776-1800):
+ * a "state" is 3 fields (u, p, gl) at stride `fs` doubles; each field holds n3+2 planes of
+ * n1*n2 doubles, i fastest: plane 0 is the ghost plane below the slab, planes 1..n3 the
+ * interior, plane n3+1 the ghost plane above.  Only ONE ghost plane is kept (the 7-point
+ * stencil reads only the first of the reference's two ghost layers, equation.c:659-724);
+ * x/y mirror and z-wall conditions are folded into the stencil's index logic.
+ */
+#ifndef PFT_HIP_H
+#define PFT_HIP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* model constants, all derived exactly as equation.c:442-447,605-612 and the left-to-right
+   products of f_GradP / f_SigmaP1_P (equation.c:367-388) */
+typedef struct {
+	double h1_2, h2_2, h3_2;         /* (n_d/L_d)^2 (global total_n3 for d = 3) */
+	double h1d2, h2d2, h3d2;         /* 0.5 * n_d/L_d */
+	double xi2a;                     /* a / (xi*xi) */
+	double bam;                      /* (b*alpha)*mu            (GradP, left-to-right prefix) */
+	double sam;                      /* (b*sqrt(0.5a)/xi*alpha)*mu (SigmaP1-P prefix) */
+	double alpha, L, zeta, u_star;
+	double p_eps0, p_eps1, e23, e32; /* Sshape limiter, 3/d^2, 2/d^3 */
+	double gamma, mhg;               /* gamma, (-0.5)*gamma */
+	double rho_g, rho_i, rho_w;
+	double cp_g, cp_i, cp_w;
+	double lam_g, lam_i, lam_w;
+	double top_temp1, top_temp2, phase_switch_time;
+} pft_consts;
+
+typedef struct pft_slab pft_slab;   /* opaque: device buffers + streams of one slab */
+
+typedef struct {
+	int n1, n2, n3;          /* interior cells of this slab */
+	int has_below;           /* 1: a neighbour slab below (ghost plane 0 is exchanged data) */
+	int has_above;           /* 1: a neighbour slab above */
+	int calc_mode;           /* 0, 1, 2, 10, 11 */
+	int gl_static;           /* 1: the model declares gl static (K_gl == 0): gl is read from x
+	                            and neither stored in K nor combined (bit-identical, F4) */
+	double eps_mult[3];      /* per-variable error multipliers (chunk_eps_mult) */
+} pft_slab_desc;
+
+/* device management */
+int pft_hip_device_count(int * n);
+int pft_hip_set_device(int dev);
+int pft_hip_get_device(int * dev);
+int pft_hip_device_sync(void);
+const char * pft_hip_last_error(void);
+
+/* slab lifecycle */
+int pft_slab_create(pft_slab ** s, const pft_slab_desc * d, const pft_consts * c);
+int pft_slab_destroy(pft_slab * s);
+size_t pft_slab_state_bytes(const pft_slab * s);
+void * pft_slab_stream(pft_slab * s);      /* hipStream_t of the compute stream */
+void * pft_slab_comm_stream(pft_slab * s); /* hipStream_t used for halo exchange */
+
+/* Buffers of a slab: X (solution), XN (candidate x(t+h)), A0/A1 (stage inputs), K1/K3/K4. */
+enum { PFT_BUF_X = 0, PFT_BUF_XN, PFT_BUF_A0, PFT_BUF_A1, PFT_BUF_K1, PFT_BUF_K3, PFT_BUF_K4, PFT_BUF_COUNT };
+double * pft_slab_buffer(pft_slab * s, int which);
+size_t pft_slab_field_stride(const pft_slab * s);     /* fs, in doubles */
+size_t pft_slab_plane(const pft_slab * s);            /* n1*n2 */
+int pft_slab_nz(const pft_slab * s);                  /* n3 (interior planes) */
+void * pft_slab_scratch(pft_slab * s);                /* device: u64 eps bits, u64 non-finite flag */
+const pft_slab_desc * pft_slab_get_desc(const pft_slab * s);
+/* planes per workgroup z-march (tuning knob, default 16) */
+int pft_slab_set_kz(pft_slab * s, int kz);
+
+/* host layout (reference padded, ghost thickness 2) <-> device layout, on the compute stream */
+int pft_slab_upload_host(pft_slab * s, int which, const double * host_padded);
+int pft_slab_download_host(pft_slab * s, int which, double * host_padded);
+
+/* One Merson stage (stage 1..5) as ONE fused kernel: K = f(stage input) and the pointwise stage
+   combine of RK_MPI_SAsolver_hybrid2.c:378-450 (stage 5: error norm :507-524 and the candidate
+   update :657-668 into XN).  t_stage: time passed to f (for the Dirichlet value);  coef: h3,
+   h6, h8, h, h3 for stages 1..5;  h: the full step (stage 4 combine);  k_begin/k_end: plane
+   range (for boundary-first splitting), -1/-1 = all planes. */
+int pft_slab_stage(pft_slab * s, int stage, double t_stage, double coef, double h,
+                   int k_begin, int k_end);
+
+/* K = f(input) only (RK_RightHandSide semantics), input/output buffer indices */
+int pft_slab_rhs(pft_slab * s, int in_buf, int out_buf, double t);
+
+/* refresh the model constants / per-variable error multipliers of an existing slab */
+int pft_slab_set_consts(pft_slab * s, const pft_consts * c);
+int pft_slab_set_eps_mult(pft_slab * s, const double * em3);
+
+/* u_noise field (PrecalculateData, equation.c:450-456), n3*n1*n2 doubles [k][j][i]; NULL clears */
+int pft_slab_set_noise(pft_slab * s, const double * host_noise);
+
+/* error norm of the last stage 5: reset before the step, fetch after (blocks on the stream) */
+int pft_slab_eps_reset(pft_slab * s);
+int pft_slab_eps_fetch(pft_slab * s, double * eps, int * nonfinite);
+
+/* HIP-event timing of the stage kernels on the compute stream (benchmark roofline):
+   mark(stage, 0|1) records the begin/end event of one stage's launches; collect() adds the
+   elapsed milliseconds of every completed begin/end pair to ms[1..5] and counts to n[1..5] */
+int pft_slab_timing_mark(pft_slab * s, int stage, int end);
+int pft_slab_timing_collect(pft_slab * s, double * ms, long * n);
+
+/* buffer swap X <-> XN after an accepted step */
+int pft_slab_accept(pft_slab * s);
+
+/* generic chunk-table combines for the host-staged path (any RK_MEM_DIST on a flat array) */
+int pft_flat_alloc(double ** p, size_t n);
+int pft_flat_free(double * p);
+int pft_flat_h2d(double * dst, const double * src, size_t n, void * stream);
+int pft_flat_d2h(double * dst, const double * src, size_t n, void * stream);
+int pft_flat_combine(int stage, int n_chunks, const int * d_start, const int * d_size,
+                     const double * d_mult, double coef, double h, const double * x,
+                     const double * k1, const double * k2, const double * k3, const double * k4,
+                     const double * k5, double * out, double * d_eps2, void * stream);
+int pft_stream_sync(void * stream);
+/* raw device memory (bytes) for the chunk tables of the host-staged path */
+int pft_dev_alloc(void ** p, size_t bytes);
+int pft_dev_free(void * p);
+int pft_h2d(void * dst, const void * src, size_t bytes, void * stream);
+
+/* peer copy of one ghost plane between slabs on the same process (loopback transport) */
+int pft_memcpy_d2d_async(void * dst, const void * src, size_t bytes, void * stream);
+int pft_event_record_wait(void * from_stream, void * to_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,56 @@
+/*
+ * pft_solver.h -- libpft extensions around the reference solver ABI (RK_MPI_SAsolver.h).
+ *
+ * RK_MPI_SA_solve() keeps the reference contract: x is a host array, mirrored host->device at
+ * entry and device->host at exit.  Drivers that keep the state on the GPU across calls (the
+ * benchmark, long runs with rare snapshots) use pft_solve_ex() with the flags below; the loop,
+ * its arithmetic and its control decisions are exactly those of RK_MPI_SA_solve().
+ */
+#ifndef PFT_SOLVER_H
+#define PFT_SOLVER_H
+
+#include "RK_MPI_SAsolver.h"
+#include "pft_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PFT_SOLVE_KEEP_DEVICE   1   /* leave x on the device at exit (no device->host copy) */
+#define PFT_SOLVE_REUSE_DEVICE  2   /* the device already holds x from the previous call */
+
+/* RK_MPI_SA_solve with an optional cap on attempted steps in this call (0 = none; returns 2
+   when the cap stops the loop, with system->t and system->h set so that the next call
+   continues the identical trajectory) and the flags above. */
+int pft_solve_ex(FLOAT final_time, RK_MPI_S_SOLUTION * system, long max_steps_total, int flags);
+
+/* copy the device-resident x back into system->x (host layout) */
+int pft_solver_download(RK_MPI_S_SOLUTION * system);
+
+enum {
+	PFT_OPT_GL_STATIC = 1,  /* 1: exploit dgl == 0 (equation.c:731,874): gl neither stored in K
+	                           nor combined -- bit-identical results, less traffic. Default 0. */
+	PFT_OPT_KZ = 2,         /* planes per workgroup z-march (default 16) */
+	PFT_OPT_DEVICE = 3,     /* HIP device of this thread's slab (default: current device) */
+	PFT_OPT_TIMING = 4      /* 1: time every stage with HIP events (stats.stage_ms) */
+};
+int pft_solver_set_option(int opt, long value);
+
+typedef struct {
+	int path;               /* 0 none yet, 1 fused device path, 2 host-staged path */
+	int nprocs, rank;
+	long kernel_launches;   /* stage kernels launched by the last call */
+	long steps_total;       /* attempted steps of the last call */
+	double last_eps;        /* max error norm of the last attempted step */
+	double stage_ms[6];     /* PFT_OPT_TIMING: summed HIP-event time of stages 1..5 */
+	long stage_n[6];        /* number of timed stage executions */
+} pft_solver_stats;
+int pft_solver_get_stats(pft_solver_stats * st);
+
+/* the slab of the fused path (benchmarks / profilers); NULL before the first fused solve */
+pft_slab * pft_solver_slab(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

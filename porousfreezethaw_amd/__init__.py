@@ -1,0 +1,286 @@
+"""porousfreezethaw_amd -- MI355X-native RK-Merson solver + intertrack freezing model.
+
+The product is the C library ``lib/libpft.so`` (host C + HIP kernels for gfx950); this module is
+a thin ctypes view of its C ABI for tests, the benchmark and scripting.  Names and argument
+meaning follow the reference's C interface (include/RK_MPI_SAsolver.h, equation.c, model.c).
+There is no CPU fallback: if the library (or a GPU, for the solving calls) is missing, the calls
+fail loudly.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "lib", "libpft.so")
+
+PARAM_NAMES = [  # model.c:44-59, the order of param[] (include/pft_model.h)
+    "u_star", "L", "xi", "a", "b", "alpha", "mu",
+    "beads_scaling", "beads_offset_x", "beads_offset_y", "beads_offset_z",
+    "xi_gl", "zeta", "p_eps0", "p_eps1", "gamma",
+    "water_cp", "ice_cp", "glass_cp", "water_lambda", "ice_lambda", "glass_lambda",
+    "water_rho", "ice_rho", "glass_rho", "top_temp1", "top_temp2", "phase_switch_time",
+    "u_noise_amp", "ball_radius",
+]
+BCOND_THICKNESS = 2
+DELTA_LOCAL, DELTA_GLOBAL = 0, 1
+RKA_CMD_FINISHED = 8
+PFT_SOLVE_KEEP_DEVICE, PFT_SOLVE_REUSE_DEVICE = 1, 2
+PFT_OPT_GL_STATIC, PFT_OPT_KZ, PFT_OPT_DEVICE, PFT_OPT_TIMING = 1, 2, 3, 4
+MPI_COMM_WORLD = 0x44000000
+
+# every function of the public headers, for the "library exports its ABI" check
+ABI_FUNCTIONS = [
+    "RK_MPI_SA_init", "RK_MPI_SA_cleanup", "RK_MPI_SA_handle_NAN", "RK_MPI_SA_check_NAN",
+    "RK_MPI_SA_check_mem", "RK_MPI_SA_solve",
+]
+
+
+class RK_MEM_DIST(C.Structure):
+    _fields_ = [("n_chunks", C.c_int), ("chunk_start", C.POINTER(C.c_int)),
+                ("chunk_size", C.POINTER(C.c_int)), ("chunk_eps_mult", C.POINTER(C.c_double))]
+
+
+RHS_FN = C.CFUNCTYPE(None, C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_double))
+META_FN = C.CFUNCTYPE(C.c_void_p)
+
+
+class RK_MPI_S_SOLUTION(C.Structure):
+    pass
+
+
+SERVICE_FN = C.CFUNCTYPE(C.c_int, C.c_double, C.POINTER(RK_MPI_S_SOLUTION))
+RK_MPI_S_SOLUTION._fields_ = [
+    ("n", C.POINTER(RK_MEM_DIST)), ("t", C.c_double), ("x", C.POINTER(C.c_double)),
+    ("meta_f", C.c_void_p), ("h", C.c_double), ("h_min", C.c_double), ("delta", C.c_double),
+    ("delta_mode", C.c_int), ("DDLBF_Rearrange", C.c_void_p), ("Service_Callback", C.c_void_p),
+    ("steps", C.c_long), ("steps_total", C.c_long)]
+
+
+class pft_grid(C.Structure):
+    _fields_ = [("n1", C.c_int), ("n2", C.c_int), ("n3", C.c_int), ("total_n3", C.c_int),
+                ("first_row", C.c_int), ("rank", C.c_int), ("nprocs", C.c_int),
+                ("L1", C.c_double), ("L2", C.c_double), ("L3", C.c_double), ("calc_mode", C.c_int)]
+
+
+class pft_solver_stats(C.Structure):
+    _fields_ = [("path", C.c_int), ("nprocs", C.c_int), ("rank", C.c_int),
+                ("kernel_launches", C.c_long), ("steps_total", C.c_long), ("last_eps", C.c_double),
+                ("stage_ms", C.c_double * 6), ("stage_n", C.c_long * 6)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libpft.so (built in-tree by __graft_entry__.build() / make -C porousfreezethaw_amd)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libpft.so is not built ({LIB_PATH}); run __graft_entry__.build()")
+        L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int)
+        L.RK_MPI_SA_init.argtypes = [C.c_int, C.c_int, C.c_int]
+        L.RK_MPI_SA_check_mem.argtypes = [C.POINTER(RK_MEM_DIST)]
+        L.RK_MPI_SA_solve.argtypes = [C.c_double, C.POINTER(RK_MPI_S_SOLUTION)]
+        L.RK_MPI_SA_handle_NAN.argtypes = [C.c_int]
+        L.RK_MPI_SA_handle_NAN.restype = None
+        L.pft_solve_ex.argtypes = [C.c_double, C.POINTER(RK_MPI_S_SOLUTION), C.c_long, C.c_int]
+        L.pft_solver_download.argtypes = [C.POINTER(RK_MPI_S_SOLUTION)]
+        L.pft_solver_set_option.argtypes = [C.c_int, C.c_long]
+        L.pft_solver_get_stats.argtypes = [C.POINTER(pft_solver_stats)]
+        L.pft_solver_slab.restype = C.c_void_p
+        L.pft_decompose.argtypes = [C.c_int, C.c_int, C.c_int, ip, ip]
+        L.pft_decompose.restype = None
+        L.pft_grid_init.argtypes = [C.POINTER(pft_grid), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                    C.c_double, C.c_double, C.c_double, C.c_int]
+        L.pft_grid_block.argtypes = [C.POINTER(pft_grid)]
+        L.pft_grid_block.restype = C.c_long
+        L.pft_model_configure.argtypes = [C.POINTER(pft_grid), dp]
+        L.bcond_setup.argtypes = [C.c_double, dp]
+        L.bcond_setup.restype = None
+        L.pft_model_set_beads.argtypes = [dp, C.c_int]
+        L.pft_model_load_beads.argtypes = [C.c_char_p]
+        L.PrecalculateData.argtypes = [dp]
+        L.pft_model_set_solution.argtypes = [dp]
+        L.pft_model_chunks.argtypes = [ip, ip, dp]
+        L.pft_model_ic_default.argtypes = [dp]
+        L.pft_float_val.argtypes = [C.c_char_p]
+        L.pft_float_val.restype = C.c_double
+        for name in ("f_generic_model01", "f_generic_model2"):
+            getattr(L, name).argtypes = [C.c_double, dp, dp]
+            getattr(L, name).restype = None
+        for name in ("mf_single", "mf_top", "mf_middle", "mf_bottom"):
+            getattr(L, name).restype = C.c_void_p
+        L.pft_hip_device_count.argtypes = [ip]
+        L.pft_hip_set_device.argtypes = [C.c_int]
+        L.pft_hip_last_error.restype = C.c_char_p
+        L.pft_comm_get_unique_id.argtypes = [C.c_void_p]
+        L.pft_comm_init_rccl.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_void_p, C.c_int]
+        L.pft_comm_init_loopback.argtypes = [C.POINTER(C.c_void_p), C.c_int]
+        L.pft_comm_loopback_rank.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
+        L.pft_comm_set_current.argtypes = [C.c_void_p]
+        L.pft_comm_destroy.argtypes = [C.c_void_p]
+        L.pft_comm_barrier.argtypes = [C.c_void_p]
+        L.pft_comm_current.restype = C.c_void_p
+        L.pft_comm_kind.argtypes = [C.c_void_p]
+        L.pft_comm_kind.restype = C.c_char_p
+        L.pft_slab_stream.argtypes = [C.c_void_p]
+        L.pft_slab_stream.restype = C.c_void_p
+        L.pft_hip_device_sync.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def _dp(a):
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _ip(a):
+    assert a.dtype == np.int32 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_int))
+
+
+def device_count():
+    n = C.c_int(0)
+    rc = lib().pft_hip_device_count(C.byref(n))
+    return n.value if rc == 0 else 0
+
+
+def decompose(total_n3, nprocs, rank):
+    n3, fr = C.c_int(), C.c_int()
+    lib().pft_decompose(total_n3, nprocs, rank, C.byref(n3), C.byref(fr))
+    return n3.value, fr.value
+
+
+def params_array(values):
+    """dict name -> value  ->  param[] in model.c order"""
+    return np.array([float(values[k]) for k in PARAM_NAMES], dtype=np.float64)
+
+
+class Simulation:
+    """One slab of an intertrack run, driven exactly like intertrack.c drives the reference.
+
+    Sets up the grid (intertrack.c:1776-1800), the host solution array and chunk table
+    (:1803-1827, :2144-2157), the model (equation.c contract), and the solver
+    (RK_MPI_SA_init :2192, check_mem :2208, PrecalculateData :2218), then solves with
+    RK_MPI_SA_solve (:2283) or the device-resident pft_solve_ex.
+    """
+
+    def __init__(self, n1, n2, total_n3, L, calc_mode, params, nprocs=1, rank=0, beads=None,
+                 initial=None, tau=1.0, tau_min=0.0, delta=1e-3, t0=0.0, gl_static=False, kz=None,
+                 init_solver=True):
+        L1, L2, L3 = L
+        self.lib = L_ = lib()
+        self.grid = pft_grid()
+        rc = L_.pft_grid_init(C.byref(self.grid), n1, n2, total_n3, nprocs, rank, L1, L2, L3, calc_mode)
+        if rc:
+            raise ValueError(f"pft_grid_init failed ({rc})")
+        self.params = np.ascontiguousarray(params, dtype=np.float64)
+        if L_.pft_model_configure(C.byref(self.grid), _dp(self.params)):
+            raise ValueError("pft_model_configure failed")
+        g = self.grid
+        self.N = (g.n3 + 4, g.n2 + 4, g.n1 + 4)
+        self.S = int(np.prod(self.N))
+        self.x = np.zeros(3 * self.S)
+        if initial is None:
+            L_.pft_model_ic_default(_dp(self.x))
+        else:
+            self.set_interior(initial)
+        nch = 3 * g.n2 * g.n3
+        self.chunk_start = np.zeros(nch, dtype=np.int32)
+        self.chunk_size = np.zeros(nch, dtype=np.int32)
+        self.chunk_mult = np.zeros(nch, dtype=np.float64)
+        L_.pft_model_chunks(_ip(self.chunk_start), _ip(self.chunk_size), _dp(self.chunk_mult))
+        self.mem = RK_MEM_DIST(nch, _ip(self.chunk_start), _ip(self.chunk_size), _dp(self.chunk_mult))
+        meta = {1: "mf_single"}.get(nprocs) or ("mf_bottom" if rank == 0 else
+                                                ("mf_top" if rank == nprocs - 1 else "mf_middle"))
+        self.meta_addr = C.cast(getattr(L_, meta), C.c_void_p).value
+        self.system = RK_MPI_S_SOLUTION(C.pointer(self.mem), t0, _dp(self.x), self.meta_addr, tau,
+                                        tau_min, delta, DELTA_GLOBAL, None, None, 0, 0)
+        L_.pft_solver_set_option(PFT_OPT_GL_STATIC, 1 if gl_static else 0)
+        if kz:
+            L_.pft_solver_set_option(PFT_OPT_KZ, kz)
+        self.initialised = False
+        if L_.AllocPrecalcData():
+            raise RuntimeError("AllocPrecalcData failed")
+        if beads is not None and initial is None:
+            b = np.ascontiguousarray(beads, dtype=np.float64)
+            L_.pft_model_set_beads(_dp(b), b.shape[0])
+            L_.pft_model_set_solution(_dp(self.x))
+        else:
+            L_.pft_model_set_solution(None)
+        if L_.PrecalculateData(_dp(self.chunk_mult)):
+            raise RuntimeError("PrecalculateData failed")
+        if init_solver:
+            rc = L_.RK_MPI_SA_init(3 * self.S, MPI_COMM_WORLD, 0)
+            if rc:
+                raise RuntimeError(f"RK_MPI_SA_init failed ({rc})")
+            self.initialised = True
+            rc = L_.RK_MPI_SA_check_mem(C.byref(self.mem))
+            if rc:
+                raise RuntimeError(f"RK_MPI_SA_check_mem failed ({rc})")
+
+    # -- host array views ------------------------------------------------------------------
+    def padded(self):
+        return self.x.reshape((3,) + self.N)
+
+    def interior(self):
+        g = self.grid
+        return np.ascontiguousarray(self.padded()[:, 2:2 + g.n3, 2:2 + g.n2, 2:2 + g.n1])
+
+    def set_interior(self, a):
+        """a: this slab's interior [3][n3][n2][n1], or the global [3][total_n3][n2][n1]"""
+        g = self.grid
+        if a.shape[1] != g.n3:
+            a = a[:, g.first_row:g.first_row + g.n3]
+        self.padded()[:, 2:2 + g.n3, 2:2 + g.n2, 2:2 + g.n1] = a
+
+    # -- solving ---------------------------------------------------------------------------
+    def solve(self, final_time):
+        rc = self.lib.RK_MPI_SA_solve(final_time, C.byref(self.system))
+        if rc < 0:
+            raise RuntimeError(f"RK_MPI_SA_solve failed ({rc}): {self.lib.pft_hip_last_error()}")
+        return rc
+
+    def solve_ex(self, final_time, max_steps_total=0, flags=0):
+        rc = self.lib.pft_solve_ex(final_time, C.byref(self.system), max_steps_total, flags)
+        if rc < 0:
+            raise RuntimeError(f"pft_solve_ex failed ({rc}): {self.lib.pft_hip_last_error()}")
+        return rc
+
+    def download(self):
+        rc = self.lib.pft_solver_download(C.byref(self.system))
+        if rc:
+            raise RuntimeError(f"pft_solver_download failed ({rc})")
+
+    def stats(self):
+        s = pft_solver_stats()
+        self.lib.pft_solver_get_stats(C.byref(s))
+        return s
+
+    @property
+    def t(self):
+        return self.system.t
+
+    @property
+    def h(self):
+        return self.system.h
+
+    def close(self):
+        if self.initialised:
+            self.lib.RK_MPI_SA_cleanup()
+            self.initialised = False
+        self.lib.FreePrecalcData()
+
+
+def rhs(sim, t, state_padded=None):
+    """K = f(t, w) through the model's RHS meta-pointer (equation.c contract) on host arrays."""
+    L_ = sim.lib
+    w = sim.x.copy() if state_padded is None else np.ascontiguousarray(state_padded, dtype=np.float64)
+    dw = np.zeros_like(w)
+    fname = "f_generic_model2" if sim.grid.calc_mode == 2 else "f_generic_model01"
+    getattr(L_, fname)(t, _dp(w), _dp(dw))
+    return dw, w

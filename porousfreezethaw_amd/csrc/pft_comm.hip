@@ -1,0 +1,324 @@
+// pft_comm.hip -- inter-slab communication for libpft (see include/pft_comm.h).
+//
+// Replaces the reference's MPI calls on the hot path (equation.c:290-326 sync_solution,
+// RK_MPI_SAsolver_hybrid2.c:572 eps Allreduce, :328-336/:616/:690 Bcasts).  Production transport:
+// RCCL (the librccl of /opt/rocm) with one process per GPU; every call is stream-ordered on the
+// slab's streams so the host never waits inside a stage.  Test transport: "loopback" -- several
+// slabs in one process (one host thread each), exchanging planes with device copies.
+#include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <rccl/rccl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/pft_comm.h"
+
+enum { KIND_SELF = 0, KIND_RCCL = 1, KIND_LOOP = 2 };
+
+struct LoopGroup {
+  int n;
+  int refs;
+  pthread_barrier_t bar;
+  pft_slab** slabs;
+  unsigned long long* eps;   // 2 per rank
+  long long* ivals;          // 1 per rank
+  char bbuf[256];
+};
+
+struct pft_comm {
+  int kind;
+  int rank, size;
+  int device;
+  pft_slab* slab;
+  ncclComm_t nccl;
+  LoopGroup* grp;
+  hipEvent_t ev_ready, ev_done;
+  int pending;
+  void* dscratch;   // 256 bytes of device memory for host-level collectives
+};
+
+static __thread pft_comm* g_current = nullptr;
+
+#define NCCLCHK(x)                                                         \
+  do {                                                                     \
+    ncclResult_t r_ = (x);                                                 \
+    if (r_ != ncclSuccess) {                                               \
+      fprintf(stderr, "pft_comm: %s failed: %s\n", #x, ncclGetErrorString(r_)); \
+      return -3000 - (int)r_;                                              \
+    }                                                                      \
+  } while (0)
+#define HCHK(x)                                                            \
+  do {                                                                     \
+    hipError_t e_ = (x);                                                   \
+    if (e_ != hipSuccess) {                                                \
+      fprintf(stderr, "pft_comm: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+      return -1000 - (int)e_;                                              \
+    }                                                                      \
+  } while (0)
+
+extern "C" {
+
+int pft_comm_init_self(pft_comm** c)
+{
+  pft_comm* m = (pft_comm*)calloc(1, sizeof(pft_comm));
+  m->kind = KIND_SELF;
+  m->size = 1;
+  *c = m;
+  return 0;
+}
+
+int pft_comm_get_unique_id(void* id_bytes)
+{
+  ncclUniqueId id;
+  NCCLCHK(ncclGetUniqueId(&id));
+  memcpy(id_bytes, &id, sizeof(id) < PFT_UNIQUE_ID_BYTES ? sizeof(id) : PFT_UNIQUE_ID_BYTES);
+  return 0;
+}
+
+int pft_comm_init_rccl(pft_comm** c, int nranks, int rank, const void* id_bytes, int device)
+{
+  *c = nullptr;
+  if (nranks < 1 || rank < 0 || rank >= nranks) return -2;
+  HCHK(hipSetDevice(device));
+  pft_comm* m = (pft_comm*)calloc(1, sizeof(pft_comm));
+  m->kind = KIND_RCCL;
+  m->rank = rank;
+  m->size = nranks;
+  m->device = device;
+  ncclUniqueId id;
+  memcpy(&id, id_bytes, sizeof(id));
+  ncclResult_t r = ncclCommInitRank(&m->nccl, nranks, id, rank);
+  if (r != ncclSuccess) {
+    fprintf(stderr, "pft_comm: ncclCommInitRank: %s\n", ncclGetErrorString(r));
+    free(m);
+    return -3000 - (int)r;
+  }
+  HCHK(hipEventCreateWithFlags(&m->ev_ready, hipEventDisableTiming));
+  HCHK(hipEventCreateWithFlags(&m->ev_done, hipEventDisableTiming));
+  HCHK(hipMalloc(&m->dscratch, 256));
+  *c = m;
+  return 0;
+}
+
+int pft_comm_init_loopback(pft_comm** group, int nranks)
+{
+  if (nranks < 1) return -2;
+  pft_comm* m = (pft_comm*)calloc(1, sizeof(pft_comm));
+  m->kind = KIND_LOOP;
+  m->rank = -1;
+  m->size = nranks;
+  LoopGroup* g = (LoopGroup*)calloc(1, sizeof(LoopGroup));
+  g->n = nranks;
+  pthread_barrier_init(&g->bar, nullptr, nranks);
+  g->slabs = (pft_slab**)calloc(nranks, sizeof(pft_slab*));
+  g->eps = (unsigned long long*)calloc(2 * nranks, sizeof(unsigned long long));
+  g->ivals = (long long*)calloc(nranks, sizeof(long long));
+  m->grp = g;
+  *group = m;
+  return 0;
+}
+
+int pft_comm_loopback_rank(pft_comm* group, int rank, pft_comm** mine)
+{
+  if (!group || group->kind != KIND_LOOP || rank < 0 || rank >= group->size) return -2;
+  pft_comm* m = (pft_comm*)calloc(1, sizeof(pft_comm));
+  m->kind = KIND_LOOP;
+  m->rank = rank;
+  m->size = group->size;
+  m->grp = group->grp;
+  __atomic_add_fetch(&m->grp->refs, 1, __ATOMIC_SEQ_CST);
+  *mine = m;
+  return 0;
+}
+
+int pft_comm_destroy(pft_comm* c)
+{
+  if (!c) return 0;
+  if (g_current == c) g_current = nullptr;
+  if (c->kind == KIND_RCCL) {
+    ncclCommDestroy(c->nccl);
+    (void)hipEventDestroy(c->ev_ready);
+    (void)hipEventDestroy(c->ev_done);
+    (void)hipFree(c->dscratch);
+  }
+  if (c->kind == KIND_LOOP && c->rank < 0) {
+    pthread_barrier_destroy(&c->grp->bar);
+    free(c->grp->slabs);
+    free(c->grp->eps);
+    free(c->grp->ivals);
+    free(c->grp);
+  }
+  free(c);
+  return 0;
+}
+
+int pft_comm_rank(const pft_comm* c) { return c ? c->rank : 0; }
+int pft_comm_size(const pft_comm* c) { return c ? c->size : 1; }
+const char* pft_comm_kind(const pft_comm* c)
+{
+  if (!c || c->kind == KIND_SELF) return "self";
+  return c->kind == KIND_RCCL ? "rccl" : "loopback";
+}
+
+int pft_comm_set_current(pft_comm* c)
+{
+  g_current = c;
+  return 0;
+}
+pft_comm* pft_comm_current(void) { return g_current; }
+
+int pft_comm_attach(pft_comm* c, pft_slab* s)
+{
+  if (!c) return -2;
+  c->slab = s;
+  if (c->kind == KIND_LOOP) c->grp->slabs[c->rank] = s;
+  return 0;
+}
+
+static void loop_barrier(pft_comm* c) { pthread_barrier_wait(&c->grp->bar); }
+
+int pft_comm_halo_start(pft_comm* c, int buf, int f0, int f1)
+{
+  if (!c || c->size == 1) return 0;
+  pft_slab* s = c->slab;
+  if (!s) return -2;
+  hipStream_t st = (hipStream_t)pft_slab_stream(s);
+  const size_t plane = pft_slab_plane(s), fs = pft_slab_field_stride(s);
+  const int n3 = pft_slab_nz(s);
+  double* b = pft_slab_buffer(s, buf);
+  const int below = c->rank > 0, above = c->rank < c->size - 1;
+  if (c->kind == KIND_RCCL) {
+    hipStream_t cs = (hipStream_t)pft_slab_comm_stream(s);
+    HCHK(hipEventRecord(c->ev_ready, st));
+    HCHK(hipStreamWaitEvent(cs, c->ev_ready, 0));
+    NCCLCHK(ncclGroupStart());
+    for (int f = f0; f < f1; ++f) {
+      double* fld = b + f * fs;
+      if (below) {
+        NCCLCHK(ncclSend(fld + 1 * plane, plane, ncclFloat64, c->rank - 1, c->nccl, cs));
+        NCCLCHK(ncclRecv(fld + 0 * plane, plane, ncclFloat64, c->rank - 1, c->nccl, cs));
+      }
+      if (above) {
+        NCCLCHK(ncclSend(fld + (size_t)n3 * plane, plane, ncclFloat64, c->rank + 1, c->nccl, cs));
+        NCCLCHK(ncclRecv(fld + (size_t)(n3 + 1) * plane, plane, ncclFloat64, c->rank + 1, c->nccl, cs));
+      }
+    }
+    NCCLCHK(ncclGroupEnd());
+    HCHK(hipEventRecord(c->ev_done, cs));
+    c->pending = 1;
+    return 0;
+  }
+  // loopback: pull the neighbours' boundary planes into our ghost planes
+  HCHK(hipStreamSynchronize(st));
+  loop_barrier(c);
+  for (int f = f0; f < f1; ++f) {
+    double* fld = b + f * fs;
+    if (below) {
+      pft_slab* nb = c->grp->slabs[c->rank - 1];
+      const double* src = pft_slab_buffer(nb, buf) + f * pft_slab_field_stride(nb) +
+                          (size_t)pft_slab_nz(nb) * pft_slab_plane(nb);
+      HCHK(hipMemcpyAsync(fld, src, plane * sizeof(double), hipMemcpyDeviceToDevice, st));
+    }
+    if (above) {
+      pft_slab* na = c->grp->slabs[c->rank + 1];
+      const double* src = pft_slab_buffer(na, buf) + f * pft_slab_field_stride(na) + pft_slab_plane(na);
+      HCHK(hipMemcpyAsync(fld + (size_t)(n3 + 1) * plane, src, plane * sizeof(double), hipMemcpyDeviceToDevice, st));
+    }
+  }
+  HCHK(hipStreamSynchronize(st));
+  loop_barrier(c);
+  return 0;
+}
+
+int pft_comm_halo_finish(pft_comm* c)
+{
+  if (!c || c->size == 1 || !c->pending) return 0;
+  c->pending = 0;
+  HCHK(hipStreamWaitEvent((hipStream_t)pft_slab_stream(c->slab), c->ev_done, 0));
+  return 0;
+}
+
+int pft_comm_halo(pft_comm* c, int buf, int f0, int f1)
+{
+  int rc = pft_comm_halo_start(c, buf, f0, f1);
+  return rc ? rc : pft_comm_halo_finish(c);
+}
+
+int pft_comm_allreduce_eps(pft_comm* c)
+{
+  if (!c || c->size == 1) return 0;
+  pft_slab* s = c->slab;
+  hipStream_t st = (hipStream_t)pft_slab_stream(s);
+  unsigned long long* d = (unsigned long long*)pft_slab_scratch(s);
+  if (c->kind == KIND_RCCL) {
+    // max of non-negative doubles == max of their bit patterns; flag: max of 0/1
+    NCCLCHK(ncclAllReduce(d, d, 2, ncclUint64, ncclMax, c->nccl, st));
+    return 0;
+  }
+  unsigned long long v[2];
+  HCHK(hipMemcpyAsync(v, d, 16, hipMemcpyDeviceToHost, st));
+  HCHK(hipStreamSynchronize(st));
+  c->grp->eps[2 * c->rank] = v[0];
+  c->grp->eps[2 * c->rank + 1] = v[1];
+  loop_barrier(c);
+  unsigned long long m0 = 0, m1 = 0;
+  for (int r = 0; r < c->size; ++r) {
+    if (c->grp->eps[2 * r] > m0) m0 = c->grp->eps[2 * r];
+    if (c->grp->eps[2 * r + 1] > m1) m1 = c->grp->eps[2 * r + 1];
+  }
+  loop_barrier(c);
+  v[0] = m0;
+  v[1] = m1;
+  HCHK(hipMemcpyAsync(d, v, 16, hipMemcpyHostToDevice, st));
+  HCHK(hipStreamSynchronize(st));
+  return 0;
+}
+
+int pft_comm_bcast(pft_comm* c, void* data, int bytes, int root)
+{
+  if (!c || c->size == 1) return 0;
+  if (bytes > 256) return -2;
+  if (c->kind == KIND_RCCL) {
+    hipStream_t st = c->slab ? (hipStream_t)pft_slab_stream(c->slab) : 0;
+    HCHK(hipMemcpyAsync(c->dscratch, data, bytes, hipMemcpyHostToDevice, st));
+    NCCLCHK(ncclBroadcast(c->dscratch, c->dscratch, bytes, ncclUint8, root, c->nccl, st));
+    HCHK(hipMemcpyAsync(data, c->dscratch, bytes, hipMemcpyDeviceToHost, st));
+    HCHK(hipStreamSynchronize(st));
+    return 0;
+  }
+  if (c->rank == root) memcpy(c->grp->bbuf, data, bytes);
+  loop_barrier(c);
+  if (c->rank != root) memcpy(data, c->grp->bbuf, bytes);
+  loop_barrier(c);
+  return 0;
+}
+
+int pft_comm_allreduce_max_i64(pft_comm* c, long long* v)
+{
+  if (!c || c->size == 1) return 0;
+  if (c->kind == KIND_RCCL) {
+    hipStream_t st = c->slab ? (hipStream_t)pft_slab_stream(c->slab) : 0;
+    HCHK(hipMemcpyAsync(c->dscratch, v, 8, hipMemcpyHostToDevice, st));
+    NCCLCHK(ncclAllReduce(c->dscratch, c->dscratch, 1, ncclInt64, ncclMax, c->nccl, st));
+    HCHK(hipMemcpyAsync(v, c->dscratch, 8, hipMemcpyDeviceToHost, st));
+    HCHK(hipStreamSynchronize(st));
+    return 0;
+  }
+  c->grp->ivals[c->rank] = *v;
+  loop_barrier(c);
+  long long m = c->grp->ivals[0];
+  for (int r = 1; r < c->size; ++r)
+    if (c->grp->ivals[r] > m) m = c->grp->ivals[r];
+  loop_barrier(c);
+  *v = m;
+  return 0;
+}
+
+int pft_comm_barrier(pft_comm* c)
+{
+  long long z = 0;
+  return pft_comm_allreduce_max_i64(c, &z);
+}
+
+}  // extern "C"

@@ -1,0 +1,757 @@
+// pft_kernels.hip -- hand-written HIP kernels for gfx950 (MI355X) + the pft_hip_* C-ABI shim.
+//
+// The hot path of RK_MPI_SA_solve (RK_MPI_SAsolver_hybrid2.c:351-766) with the intertrack
+// right-hand side (equation.c:566-884) fused per Merson stage: each stage is ONE kernel that
+// evaluates the 7-point RHS at a cell and immediately applies that stage's pointwise combine
+// (hybrid2.c:378-450), the error norm (:507-524) and the candidate update (:657-668).  Every
+// floating-point operation is the reference's, in the reference's order, with contraction
+// disabled (-ffp-contract=off and the pragma below), so results are bit-identical to the CPU
+// reference for calc_mode 0/1/10/11 (mode 2 differs only through device cosh, <= 1 ulp).
+//
+// Memory: per slab, a field is (n3+2) planes of n1*n2 doubles (one ghost plane each side, filled
+// only at slab interfaces).  Mirror / Dirichlet walls (equation.c:113-263) are folded into the
+// neighbour selection: the first mirrored ghost equals the boundary cell itself.
+//
+// Launch geometry: a 256-thread workgroup owns 256 consecutive (i,j) columns of the flattened
+// plane (fully coalesced 2 KiB loads) and marches `kz` planes in z with the z-neighbours of all
+// three fields in registers (2.5-D blocking).  x/y neighbours come from the L1/L2; the linear
+// workgroup id is remapped so that the 8 XCDs each take a contiguous run of tiles (their y
+// neighbours then share the XCD's L2, cdna_hip_programming.md T1).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/pft_hip.h"
+
+#pragma clang fp contract(off)
+
+#define PFT_BLOCK 256
+
+static __thread char g_err[256];
+
+static int fail(hipError_t e, const char* what)
+{
+  snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+  return -(int)e - 1000;
+}
+#define HIPCHK(x)                                  \
+  do {                                             \
+    hipError_t e_ = (x);                           \
+    if (e_ != hipSuccess) return fail(e_, #x);     \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------
+// model arithmetic (equation.c:330-421, 650-731, 835-874), operation order preserved
+
+struct Col {           // one field at a cell: centre and its 6 face neighbours
+  double c, xm, xp, ym, yp, zm, zp;
+};
+
+__device__ __forceinline__ double lam_of(const pft_consts& c, double p, double g)
+{
+  return g * c.lam_g + (1.0 - g) * (p * c.lam_i + (1.0 - p) * c.lam_w);
+}
+
+__device__ __forceinline__ double sshape(const pft_consts& c, double x)
+{
+  if (x <= c.p_eps0) return 0.0;
+  if (x >= c.p_eps1) return 1.0;
+  x -= c.p_eps0;
+  return x * x * (c.e23 - c.e32 * x);
+}
+
+// K (du, dp) at one cell; dgl is identically 0 (equation.c:731,874)
+template <int MODE>
+__device__ __forceinline__ void rhs_cell(const pft_consts& c, const Col& u, const Col& p, const Col& g,
+                                         double un, double& du, double& dp)
+{
+  // un = u + u_noise (equation.c:676,687); only the reaction terms see the noise
+  const double pc = p.c, gc = g.c, uc = u.c;
+  const double rho = gc * c.rho_g + (1.0 - gc) * (pc * c.rho_i + (1.0 - pc) * c.rho_w);
+  const double cp = gc * c.cp_g + (1.0 - gc) * (pc * c.cp_i + (1.0 - pc) * c.cp_w);
+  const double wi = fmax(0.0, 1.0 - c.zeta * gc);
+  if (MODE == 10 || MODE == 11) {
+    du = 0.0;
+  }
+  double flux = 0.0;
+  if (MODE != 10 && MODE != 11) {
+    const double lxm = lam_of(c, 0.5 * (p.xm + pc), 0.5 * (g.xm + gc));
+    const double lxp = lam_of(c, 0.5 * (pc + p.xp), 0.5 * (gc + g.xp));
+    const double lym = lam_of(c, 0.5 * (p.ym + pc), 0.5 * (g.ym + gc));
+    const double lyp = lam_of(c, 0.5 * (pc + p.yp), 0.5 * (gc + g.yp));
+    const double lzm = lam_of(c, 0.5 * (p.zm + pc), 0.5 * (g.zm + gc));
+    const double lzp = lam_of(c, 0.5 * (pc + p.zp), 0.5 * (gc + g.zp));
+    flux = c.h1_2 * (-lxm * (-u.xm + uc) + lxp * (-uc + u.xp)) +
+           c.h2_2 * (-lym * (-u.ym + uc) + lyp * (-uc + u.yp)) +
+           c.h3_2 * (-lzm * (-u.zm + uc) + lzp * (-uc + u.zp));
+  }
+  if (MODE == 2) {
+    const double ch = cosh(c.gamma * (uc - c.u_star));
+    const double dpdu = (c.mhg / (ch * ch)) * wi;
+    const double d = flux / (rho * (cp - c.L * dpdu));
+    du = d;
+    dp = dpdu * d;
+  } else {
+    double dpdt = c.h1_2 * (-(-p.xm + pc) + (-pc + p.xp)) +
+                  c.h2_2 * (-(-p.ym + pc) + (-pc + p.yp)) +
+                  c.h3_2 * (-(-p.zm + pc) + (-pc + p.zp));
+    if (MODE == 0 || MODE == 10) {
+      const double v1 = c.h1d2 * (-p.xm + p.xp);
+      const double v2 = c.h2d2 * (-p.ym + p.yp);
+      const double v3 = c.h3d2 * (-p.zm + p.zp);
+      const double gn = sqrt(v1 * v1 + v2 * v2 + v3 * v3) + 1E-10;
+      dpdt += c.xi2a * pc * (1.0 - pc) * (pc - 0.5) - c.bam * gn * (un - c.u_star);
+    } else {
+      dpdt += c.xi2a * pc * (1.0 - pc) * (pc - 0.5) -
+              c.sam * sshape(c, pc) * sshape(c, 1.0 - pc) * fmax(pc * (1.0 - pc), 0.0) * (un - c.u_star);
+    }
+    dpdt /= c.alpha;
+    dpdt *= wi;
+    dp = dpdt;
+    if (MODE == 0 || MODE == 1) du = (flux / rho + c.L * dpdt) / cp;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// the fused stage kernel
+
+struct StageArgs {
+  const double* in;    // stage input state (u, p, gl)
+  const double* x;     // solution x
+  const double* k1;
+  const double* k3;
+  const double* k4;
+  double* kout;        // K of this stage (stages 0, 1, 3, 4)
+  double* out;         // next stage input (1..4) or candidate x(t+h) (5)
+  unsigned long long* eps_bits;
+  unsigned int* nonfinite;
+  const double* noise; // u_noise [k][j][i] or null (u_noise_amp == 0)
+  long fs;             // field stride (doubles)
+  int n1, n2, n3, plane;
+  int has_below, has_above;
+  int k_begin, k_end, kz, ntile, nchunk;
+  double T_top;        // Dirichlet value T_top(t_stage), equation.c:110
+  double coef, h;
+  double em0, em1, em2;
+};
+
+__device__ __forceinline__ int xcd_remap(int b, int n)
+{
+  // bijective: the blocks the dispatcher deals to one XCD (b % 8 equal) get consecutive ids
+  const int q = n >> 3, r = n & 7, x = b & 7, l = b >> 3;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + l;
+}
+
+template <int STAGE, bool GLS>
+__device__ __forceinline__ double combine(const StageArgs& a, int q, long o, double K, double* m, bool& nf)
+{
+  // returns the value written to `out` (not used for stage 0)
+  const double xv = a.x[q * a.fs + o];
+  if (STAGE == 1) {
+    a.kout[q * a.fs + o] = K;
+    a.out[q * a.fs + o] = K * a.coef + xv;                               // hybrid2.c:388
+  } else if (STAGE == 2) {
+    const double k1 = a.k1[q * a.fs + o];
+    a.out[q * a.fs + o] = (k1 + K) * a.coef + xv;                        // :408
+  } else if (STAGE == 3) {
+    const double k1 = a.k1[q * a.fs + o];
+    a.kout[q * a.fs + o] = K;
+    a.out[q * a.fs + o] = (k1 + 3.0 * K) * a.coef + xv;                  // :428
+  } else if (STAGE == 4) {
+    const double k1 = a.k1[q * a.fs + o], k3 = a.k3[q * a.fs + o];
+    a.kout[q * a.fs + o] = K;
+    a.out[q * a.fs + o] = (0.5 * k1 - 1.5 * k3 + 2.0 * K) * a.h + xv;   // :449
+  } else if (STAGE == 5) {
+    const double k1 = a.k1[q * a.fs + o], k3 = a.k3[q * a.fs + o], k4 = a.k4[q * a.fs + o];
+    const double em = q == 0 ? a.em0 : (q == 1 ? a.em1 : a.em2);
+    const double e = em * fabs(0.2 * k1 - 0.9 * k3 + 0.8 * k4 - 0.1 * K);   // :521
+    if (e > *m) *m = e;                                                  // :522 (NaN never wins)
+    nf |= !isfinite(e);
+    a.out[q * a.fs + o] = xv + a.coef * (0.5 * (k1 + K) + 2.0 * k4);   // :667
+  }
+  return 0.0;
+}
+
+template <int STAGE, int MODE, bool GLS>
+__global__ __launch_bounds__(PFT_BLOCK) void merson_stage(StageArgs a, pft_consts c)
+{
+  const int lin = xcd_remap(blockIdx.x, a.ntile * a.nchunk);
+  const int tile = lin % a.ntile, chunk = lin / a.ntile;
+  const int cell = tile * PFT_BLOCK + threadIdx.x;
+  const bool active = cell < a.plane;
+  const int cc = active ? cell : a.plane - 1;
+  const int j = cc / a.n1, i = cc - j * a.n1;
+  const int kb = a.k_begin + chunk * a.kz;
+  const int ke = min(kb + a.kz, a.k_end);
+
+  // neighbour offsets within a plane, mirrored at the x/y walls (equation.c:137-161)
+  const int oxm = i > 0 ? -1 : 0, oxp = i < a.n1 - 1 ? 1 : 0;
+  const int oym = j > 0 ? -a.n1 : 0, oyp = j < a.n2 - 1 ? a.n1 : 0;
+
+  const double* fin[3] = {a.in, a.in + a.fs, GLS ? a.x + 2 * a.fs : a.in + 2 * a.fs};
+
+  double m = 0.0;
+  bool nf = false;
+  double zm[3], zc[3], zp[3];
+  if (kb < ke) {
+    const long o0 = (long)(kb + 1) * a.plane + cc;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      zc[q] = fin[q][o0];
+      // bottom wall: mirror (equation.c:164-174); slab interface: ghost plane
+      zm[q] = (kb == 0 && !a.has_below) ? zc[q] : fin[q][o0 - a.plane];
+    }
+  }
+  for (int k = kb; k < ke; ++k) {
+    const long o = (long)(k + 1) * a.plane + cc;
+    const bool top = (k == a.n3 - 1) && !a.has_above;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) zp[q] = top ? zc[q] : fin[q][o + a.plane];
+    if (top) zp[0] = a.T_top;                       // Dirichlet u (equation.c:175-183)
+    Col col[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      col[q].c = zc[q];
+      col[q].xm = fin[q][o + oxm];
+      col[q].xp = fin[q][o + oxp];
+      col[q].ym = fin[q][o + oym];
+      col[q].yp = fin[q][o + oyp];
+      col[q].zm = zm[q];
+      col[q].zp = zp[q];
+    }
+    double du = 0.0, dp = 0.0;
+    const double un = a.noise ? zc[0] + a.noise[(long)k * a.plane + cc] : zc[0];
+    rhs_cell<MODE>(c, col[0], col[1], col[2], un, du, dp);
+    if (active) {
+      if (STAGE == 0) {
+        a.kout[o] = du;
+        a.kout[a.fs + o] = dp;
+        a.kout[2 * a.fs + o] = 0.0;
+      } else {
+        combine<STAGE, GLS>(a, 0, o, du, &m, nf);
+        combine<STAGE, GLS>(a, 1, o, dp, &m, nf);
+        if (!GLS) combine<STAGE, GLS>(a, 2, o, 0.0, &m, nf);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      zm[q] = zc[q];
+      zc[q] = zp[q];
+    }
+  }
+
+  if (STAGE == 5) {
+    // block max of the error norm (exact, order-independent), one atomic per block
+    __shared__ double red[PFT_BLOCK / 64];
+    __shared__ int rnf[PFT_BLOCK / 64];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double o = __shfl_xor(m, off, 64);
+      if (o > m) m = o;
+    }
+    const int anynf = __any(nf);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+      red[w] = m;
+      rnf[w] = anynf;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double bm = red[0];
+      int bnf = rnf[0];
+      for (int k = 1; k < PFT_BLOCK / 64; ++k) {
+        if (red[k] > bm) bm = red[k];
+        bnf |= rnf[k];
+      }
+      // non-negative doubles order like their bit patterns
+      if (bm > 0.0) atomicMax(a.eps_bits, (unsigned long long)__double_as_longlong(bm));
+      if (bnf) atomicOr(a.nonfinite, 1u);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// layout conversion kernels (host padded layout, ghost thickness 2 <-> device layout)
+
+__global__ void pack_kernel(const double* __restrict__ host, double* __restrict__ dev, int n1, int n2,
+                            int n3, long fs, long S)
+{
+  // planes -1..n3 of every field (ghost planes included)
+  const long plane = (long)n1 * n2;
+  const long total = 3L * (n3 + 2) * plane;
+  const int N1 = n1 + 4, N2 = n2 + 4;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int q = (int)(e / ((n3 + 2) * plane));
+    const long r = e - (long)q * (n3 + 2) * plane;
+    const int kk = (int)(r / plane);          // 0..n3+1 = k+1
+    const long c = r - (long)kk * plane;
+    const int j = (int)(c / n1), i = (int)(c - (long)j * n1);
+    dev[q * fs + r] = host[q * S + (long)(kk + 1) * N1 * N2 + (long)(j + 2) * N1 + (i + 2)];
+  }
+}
+
+__global__ void unpack_kernel(const double* __restrict__ dev, double* __restrict__ host, int n1, int n2,
+                              int n3, long fs, long S)
+{
+  // interior planes only
+  const long plane = (long)n1 * n2;
+  const long total = 3L * n3 * plane;
+  const int N1 = n1 + 4, N2 = n2 + 4;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int q = (int)(e / (n3 * plane));
+    const long r = e - (long)q * n3 * plane;
+    const int k = (int)(r / plane);
+    const long c = r - (long)k * plane;
+    const int j = (int)(c / n1), i = (int)(c - (long)j * n1);
+    host[q * S + (long)(k + 2) * N1 * N2 + (long)(j + 2) * N1 + (i + 2)] = dev[q * fs + (long)(k + 1) * plane + c];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// generic chunk-table combines (host-staged path for unregistered right-hand sides)
+
+__global__ void flat_combine_kernel(int stage, int n_chunks, const int* __restrict__ cstart,
+                                    const int* __restrict__ csize, const double* __restrict__ cmult,
+                                    double coef, double h, const double* x, const double* k1,
+                                    const double* k2, const double* k3, const double* k4,
+                                    const double* k5, double* out, unsigned long long* eps_bits,
+                                    unsigned int* nonfinite)
+{
+  double m = 0.0;
+  bool nf = false;
+  for (int ch = blockIdx.x; ch < n_chunks; ch += gridDim.x) {
+    const long s0 = cstart[ch];
+    const int n = csize[ch];
+    const double mult = cmult ? cmult[ch] : 1.0;
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+      const long e = s0 + t;
+      switch (stage) {
+        case 1: out[e] = k1[e] * coef + x[e]; break;                              // :388
+        case 2: out[e] = (k1[e] + k2[e]) * coef + x[e]; break;                    // :408
+        case 3: out[e] = (k1[e] + 3.0 * k3[e]) * coef + x[e]; break;              // :428
+        case 4: out[e] = (0.5 * k1[e] - 1.5 * k3[e] + 2.0 * k4[e]) * h + x[e]; break;  // :449
+        case 5: {
+          const double ev = mult * fabs(0.2 * k1[e] - 0.9 * k3[e] + 0.8 * k4[e] - 0.1 * k5[e]);
+          if (ev > m) m = ev;
+          nf |= !isfinite(ev);
+        } break;
+        case 6: out[e] += coef * (0.5 * (k1[e] + k5[e]) + 2.0 * k4[e]); break;    // :667
+      }
+    }
+  }
+  if (stage == 5) {
+    __shared__ double red[PFT_BLOCK / 64];
+    __shared__ int rnf[PFT_BLOCK / 64];
+    for (int off = 32; off > 0; off >>= 1) {
+      const double o = __shfl_xor(m, off, 64);
+      if (o > m) m = o;
+    }
+    const int anynf = __any(nf);
+    if ((threadIdx.x & 63) == 0) {
+      red[threadIdx.x >> 6] = m;
+      rnf[threadIdx.x >> 6] = anynf;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double bm = red[0];
+      int bnf = rnf[0];
+      for (int k = 1; k < (int)(blockDim.x / 64); ++k) {
+        if (red[k] > bm) bm = red[k];
+        bnf |= rnf[k];
+      }
+      if (bm > 0.0) atomicMax(eps_bits, (unsigned long long)__double_as_longlong(bm));
+      if (bnf) atomicOr(nonfinite, 1u);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// slab object + shim
+
+struct pft_slab {
+  pft_slab_desc d;
+  pft_consts c;
+  long fs;
+  int plane;
+  double* buf[PFT_BUF_COUNT];
+  double* staging;       // host padded layout on the device (for upload/download)
+  long S;                // host padded block (one field)
+  unsigned long long* scratch;  // [0] eps bits, [1] nonfinite flag
+  unsigned long long* host_scratch;  // pinned
+  hipStream_t stream, comm;
+  int kz;
+  double* noise;         // device u_noise (n3*plane) or null
+  hipEvent_t tev[6][2];  // per-stage timing events
+  int tpending[6];
+};
+
+extern "C" {
+
+const char* pft_hip_last_error(void) { return g_err; }
+
+int pft_hip_device_count(int* n)
+{
+  HIPCHK(hipGetDeviceCount(n));
+  return 0;
+}
+int pft_hip_set_device(int dev)
+{
+  HIPCHK(hipSetDevice(dev));
+  return 0;
+}
+int pft_hip_get_device(int* dev)
+{
+  HIPCHK(hipGetDevice(dev));
+  return 0;
+}
+int pft_hip_device_sync(void)
+{
+  HIPCHK(hipDeviceSynchronize());
+  return 0;
+}
+
+int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
+{
+  *out = nullptr;
+  if (d->n1 < 1 || d->n2 < 1 || d->n3 < 1) return -2;
+  pft_slab* s = new pft_slab();
+  memset(s, 0, sizeof(*s));
+  s->d = *d;
+  s->c = *c;
+  s->plane = d->n1 * d->n2;
+  const long raw = (long)(d->n3 + 2) * s->plane;
+  s->fs = (raw + 63) & ~63L;  // 512-byte aligned field starts
+  s->S = (long)(d->n1 + 4) * (d->n2 + 4) * (d->n3 + 4);
+  s->kz = 16;
+  const size_t bytes = sizeof(double) * 3 * (size_t)s->fs;
+  for (int b = 0; b < PFT_BUF_COUNT; ++b) {
+    hipError_t e = hipMalloc((void**)&s->buf[b], bytes);
+    if (e != hipSuccess) {
+      pft_slab_destroy(s);
+      return fail(e, "hipMalloc(state)");
+    }
+    e = hipMemset(s->buf[b], 0, bytes);
+    if (e != hipSuccess) {
+      pft_slab_destroy(s);
+      return fail(e, "hipMemset(state)");
+    }
+  }
+  hipError_t e = hipMalloc((void**)&s->scratch, 64);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&s->host_scratch, 64, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->comm, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    pft_slab_destroy(s);
+    return fail(e, "slab scratch/streams");
+  }
+  *out = s;
+  return 0;
+}
+
+int pft_slab_destroy(pft_slab* s)
+{
+  if (!s) return 0;
+  for (int b = 0; b < PFT_BUF_COUNT; ++b)
+    if (s->buf[b]) (void)hipFree(s->buf[b]);
+  if (s->staging) (void)hipFree(s->staging);
+  if (s->noise) (void)hipFree(s->noise);
+  for (int st = 0; st < 6; ++st)
+    for (int e = 0; e < 2; ++e)
+      if (s->tev[st][e]) (void)hipEventDestroy(s->tev[st][e]);
+  if (s->scratch) (void)hipFree(s->scratch);
+  if (s->host_scratch) (void)hipHostFree(s->host_scratch);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  if (s->comm) (void)hipStreamDestroy(s->comm);
+  delete s;
+  return 0;
+}
+
+size_t pft_slab_state_bytes(const pft_slab* s) { return sizeof(double) * 3 * (size_t)s->fs; }
+void* pft_slab_stream(pft_slab* s) { return (void*)s->stream; }
+void* pft_slab_comm_stream(pft_slab* s) { return (void*)s->comm; }
+double* pft_slab_buffer(pft_slab* s, int which) { return (which >= 0 && which < PFT_BUF_COUNT) ? s->buf[which] : nullptr; }
+size_t pft_slab_field_stride(const pft_slab* s) { return (size_t)s->fs; }
+size_t pft_slab_plane(const pft_slab* s) { return (size_t)s->plane; }
+int pft_slab_nz(const pft_slab* s) { return s->d.n3; }
+void* pft_slab_scratch(pft_slab* s) { return (void*)s->scratch; }
+const pft_slab_desc* pft_slab_get_desc(const pft_slab* s) { return &s->d; }
+int pft_slab_set_kz(pft_slab* s, int kz)
+{
+  if (kz < 1) return -2;
+  s->kz = kz;
+  return 0;
+}
+
+static int ensure_staging(pft_slab* s)
+{
+  if (s->staging) return 0;
+  HIPCHK(hipMalloc((void**)&s->staging, sizeof(double) * 3 * (size_t)s->S));
+  return 0;
+}
+
+int pft_slab_upload_host(pft_slab* s, int which, const double* host_padded)
+{
+  int rc = ensure_staging(s);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(s->staging, host_padded, sizeof(double) * 3 * (size_t)s->S, hipMemcpyHostToDevice,
+                        s->stream));
+  pack_kernel<<<2048, 256, 0, s->stream>>>(s->staging, s->buf[which], s->d.n1, s->d.n2, s->d.n3, s->fs, s->S);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+int pft_slab_download_host(pft_slab* s, int which, double* host_padded)
+{
+  int rc = ensure_staging(s);
+  if (rc) return rc;
+  // staging keeps the host's ghost values (copied in first), interior overwritten
+  HIPCHK(hipMemcpyAsync(s->staging, host_padded, sizeof(double) * 3 * (size_t)s->S, hipMemcpyHostToDevice,
+                        s->stream));
+  unpack_kernel<<<2048, 256, 0, s->stream>>>(s->buf[which], s->staging, s->d.n1, s->d.n2, s->d.n3, s->fs, s->S);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(host_padded, s->staging, sizeof(double) * 3 * (size_t)s->S, hipMemcpyDeviceToHost,
+                        s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return 0;
+}
+
+}  // extern "C"
+
+template <int STAGE, bool GLS>
+static void launch_mode(int mode, dim3 g, hipStream_t st, const StageArgs& a, const pft_consts& c)
+{
+  switch (mode) {
+    case 0: merson_stage<STAGE, 0, GLS><<<g, PFT_BLOCK, 0, st>>>(a, c); break;
+    case 1: merson_stage<STAGE, 1, GLS><<<g, PFT_BLOCK, 0, st>>>(a, c); break;
+    case 2: merson_stage<STAGE, 2, GLS><<<g, PFT_BLOCK, 0, st>>>(a, c); break;
+    case 10: merson_stage<STAGE, 10, GLS><<<g, PFT_BLOCK, 0, st>>>(a, c); break;
+    case 11: merson_stage<STAGE, 11, GLS><<<g, PFT_BLOCK, 0, st>>>(a, c); break;
+  }
+}
+
+template <bool GLS>
+static void launch_stage(int stage, int mode, dim3 g, hipStream_t st, const StageArgs& a, const pft_consts& c)
+{
+  switch (stage) {
+    case 0: launch_mode<0, GLS>(mode, g, st, a, c); break;
+    case 1: launch_mode<1, GLS>(mode, g, st, a, c); break;
+    case 2: launch_mode<2, GLS>(mode, g, st, a, c); break;
+    case 3: launch_mode<3, GLS>(mode, g, st, a, c); break;
+    case 4: launch_mode<4, GLS>(mode, g, st, a, c); break;
+    case 5: launch_mode<5, GLS>(mode, g, st, a, c); break;
+  }
+}
+
+extern "C" {
+
+static int run_stage(pft_slab* s, int stage, const double* in, double* kout, double* out, double t_stage,
+                     double coef, double h, int k_begin, int k_end, int gls)
+{
+  const int mode = s->d.calc_mode;
+  if (mode != 0 && mode != 1 && mode != 2 && mode != 10 && mode != 11) return -2;
+  if (k_begin < 0) k_begin = 0;
+  if (k_end < 0 || k_end > s->d.n3) k_end = s->d.n3;
+  if (k_end <= k_begin) return 0;
+  StageArgs a;
+  memset(&a, 0, sizeof(a));
+  a.in = in;
+  a.x = s->buf[PFT_BUF_X];
+  a.k1 = s->buf[PFT_BUF_K1];
+  a.k3 = s->buf[PFT_BUF_K3];
+  a.k4 = s->buf[PFT_BUF_K4];
+  a.kout = kout;
+  a.out = out;
+  a.noise = s->noise;
+  a.eps_bits = s->scratch;
+  a.nonfinite = (unsigned int*)(s->scratch + 1);
+  a.fs = s->fs;
+  a.n1 = s->d.n1;
+  a.n2 = s->d.n2;
+  a.n3 = s->d.n3;
+  a.plane = s->plane;
+  a.has_below = s->d.has_below;
+  a.has_above = s->d.has_above;
+  a.k_begin = k_begin;
+  a.k_end = k_end;
+  a.kz = s->kz;
+  a.ntile = (s->plane + PFT_BLOCK - 1) / PFT_BLOCK;
+  a.nchunk = (k_end - k_begin + a.kz - 1) / a.kz;
+  a.T_top = t_stage < s->c.phase_switch_time ? s->c.top_temp1 : s->c.top_temp2;
+  a.coef = coef;
+  a.h = h;
+  a.em0 = s->d.eps_mult[0];
+  a.em1 = s->d.eps_mult[1];
+  a.em2 = s->d.eps_mult[2];
+  dim3 g((unsigned)(a.ntile * a.nchunk));
+  if (gls)
+    launch_stage<true>(stage, mode, g, s->stream, a, s->c);
+  else
+    launch_stage<false>(stage, mode, g, s->stream, a, s->c);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int pft_slab_stage(pft_slab* s, int stage, double t_stage, double coef, double h, int k_begin, int k_end)
+{
+  // buffer rotation of the fused step: in -> (kout, out)
+  static const int in_of[6] = {-1, PFT_BUF_X, PFT_BUF_A0, PFT_BUF_A1, PFT_BUF_A0, PFT_BUF_A1};
+  static const int out_of[6] = {-1, PFT_BUF_A0, PFT_BUF_A1, PFT_BUF_A0, PFT_BUF_A1, PFT_BUF_XN};
+  static const int k_of[6] = {-1, PFT_BUF_K1, -1, PFT_BUF_K3, PFT_BUF_K4, -1};
+  if (stage < 1 || stage > 5) return -2;
+  return run_stage(s, stage, s->buf[in_of[stage]], k_of[stage] >= 0 ? s->buf[k_of[stage]] : nullptr,
+                   s->buf[out_of[stage]], t_stage, coef, h, k_begin, k_end, s->d.gl_static);
+}
+
+int pft_slab_rhs(pft_slab* s, int in_buf, int out_buf, double t)
+{
+  if (in_buf < 0 || in_buf >= PFT_BUF_COUNT || out_buf < 0 || out_buf >= PFT_BUF_COUNT) return -2;
+  return run_stage(s, 0, s->buf[in_buf], s->buf[out_buf], nullptr, t, 0.0, 0.0, -1, -1, 0);
+}
+
+int pft_slab_set_consts(pft_slab* s, const pft_consts* c)
+{
+  s->c = *c;
+  return 0;
+}
+
+int pft_slab_set_eps_mult(pft_slab* s, const double* em3)
+{
+  for (int q = 0; q < 3; ++q) s->d.eps_mult[q] = em3[q];
+  return 0;
+}
+
+int pft_slab_set_noise(pft_slab* s, const double* host_noise)
+{
+  if (!host_noise) {
+    if (s->noise) HIPCHK(hipFree(s->noise));
+    s->noise = nullptr;
+    return 0;
+  }
+  const size_t bytes = sizeof(double) * (size_t)s->plane * s->d.n3;
+  if (!s->noise) HIPCHK(hipMalloc((void**)&s->noise, bytes));
+  HIPCHK(hipMemcpy(s->noise, host_noise, bytes, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int pft_slab_eps_reset(pft_slab* s)
+{
+  HIPCHK(hipMemsetAsync(s->scratch, 0, 16, s->stream));
+  return 0;
+}
+
+int pft_slab_eps_fetch(pft_slab* s, double* eps, int* nonfinite)
+{
+  HIPCHK(hipMemcpyAsync(s->host_scratch, s->scratch, 16, hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  unsigned long long b = s->host_scratch[0];
+  double v;
+  memcpy(&v, &b, 8);
+  *eps = v;
+  if (nonfinite) *nonfinite = (int)(s->host_scratch[1] & 0xffffffffu);
+  return 0;
+}
+
+int pft_slab_timing_mark(pft_slab* s, int stage, int end)
+{
+  if (stage < 1 || stage > 5) return -2;
+  if (!s->tev[stage][0]) {
+    HIPCHK(hipEventCreate(&s->tev[stage][0]));
+    HIPCHK(hipEventCreate(&s->tev[stage][1]));
+  }
+  HIPCHK(hipEventRecord(s->tev[stage][end ? 1 : 0], s->stream));
+  if (end) s->tpending[stage] = 1;
+  return 0;
+}
+
+int pft_slab_timing_collect(pft_slab* s, double* ms, long* n)
+{
+  for (int st = 1; st <= 5; ++st) {
+    if (!s->tpending[st]) continue;
+    float e = 0.f;
+    HIPCHK(hipEventSynchronize(s->tev[st][1]));
+    HIPCHK(hipEventElapsedTime(&e, s->tev[st][0], s->tev[st][1]));
+    ms[st] += (double)e;
+    n[st] += 1;
+    s->tpending[st] = 0;
+  }
+  return 0;
+}
+
+int pft_slab_accept(pft_slab* s)
+{
+  double* t = s->buf[PFT_BUF_X];
+  s->buf[PFT_BUF_X] = s->buf[PFT_BUF_XN];
+  s->buf[PFT_BUF_XN] = t;
+  return 0;
+}
+
+int pft_flat_alloc(double** p, size_t n)
+{
+  HIPCHK(hipMalloc((void**)p, n * sizeof(double)));
+  return 0;
+}
+int pft_flat_free(double* p)
+{
+  if (p) HIPCHK(hipFree(p));
+  return 0;
+}
+int pft_flat_h2d(double* dst, const double* src, size_t n, void* stream)
+{
+  HIPCHK(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyHostToDevice, (hipStream_t)stream));
+  return 0;
+}
+int pft_flat_d2h(double* dst, const double* src, size_t n, void* stream)
+{
+  HIPCHK(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToHost, (hipStream_t)stream));
+  return 0;
+}
+int pft_flat_combine(int stage, int n_chunks, const int* d_start, const int* d_size, const double* d_mult,
+                     double coef, double h, const double* x, const double* k1, const double* k2, const double* k3,
+                     const double* k4, const double* k5, double* out, double* d_eps2, void* stream)
+{
+  const int blocks = n_chunks < 4096 ? n_chunks : 4096;
+  if (blocks <= 0) return -2;
+  flat_combine_kernel<<<blocks, PFT_BLOCK, 0, (hipStream_t)stream>>>(
+      stage, n_chunks, d_start, d_size, d_mult, coef, h, x, k1, k2, k3, k4, k5, out,
+      (unsigned long long*)d_eps2, (unsigned int*)(d_eps2 + 1));
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+int pft_stream_sync(void* stream)
+{
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  return 0;
+}
+int pft_dev_alloc(void** p, size_t bytes)
+{
+  HIPCHK(hipMalloc(p, bytes));
+  return 0;
+}
+int pft_dev_free(void* p)
+{
+  if (p) HIPCHK(hipFree(p));
+  return 0;
+}
+int pft_h2d(void* dst, const void* src, size_t bytes, void* stream)
+{
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+  return 0;
+}
+int pft_memcpy_d2d_async(void* dst, const void* src, size_t bytes, void* stream)
+{
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return 0;
+}
+int pft_event_record_wait(void* from_stream, void* to_stream)
+{
+  hipEvent_t e;
+  HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(e, (hipStream_t)from_stream));
+  HIPCHK(hipStreamWaitEvent((hipStream_t)to_stream, e, 0));
+  HIPCHK(hipEventDestroy(e));
+  return 0;
+}
+
+}  // extern "C"

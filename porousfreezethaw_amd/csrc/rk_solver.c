@@ -1,0 +1,549 @@
+/*
+ * rk_solver.c -- libpft's RK_MPI_SAsolver ABI (include/RK_MPI_SAsolver.h): the adaptive
+ * 4th-order Runge-Kutta-Merson solver of modules/RK_MPI_SAsolver_hybrid2/RK_MPI_SAsolver_hybrid2.c
+ * (and its twin _hybrid), re-designed for MI355X.
+ *
+ * Host C.  The control logic -- step size, accept/reject, finish/next-finish, NaN retries,
+ * service callback, meta-pointer refresh, return codes -- is restated line for line from
+ * hybrid2.c:215-770 (citations inline); every decision uses the same fp64 expressions, so
+ * trajectories are identical to the reference's.  The array work runs on the GPU:
+ *
+ *  - fused path (the hot path): when meta_f() returns libpft's intertrack right-hand side and
+ *    the chunk table is the driver's canonical one (intertrack.c:2144-2157), x lives on the
+ *    device and each attempted step is 5 fused stage kernels (pft_kernels.hip) + one 16-byte
+ *    device->host read of the global error norm; with several ranks the stage outputs' boundary
+ *    planes travel by RCCL while the interior planes are computed (pft_comm.h).
+ *  - host-staged path: any other RK_RightHandSide is called on the host with host arrays; the
+ *    stage combines, the error norm and the update run as HIP kernels over the chunk table.
+ *
+ * Solver state is per host thread (the reference's is per MPI process: one static instance).
+ */
+#include "pft_internal.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct {
+	int max_n;                    /* hybrid2.c:61; 0 = not initialised */
+	int master;
+	int handle_nan, last_nan;     /* :63-64 */
+	pft_comm * self_comm;
+	/* fused path */
+	pft_slab * slab;
+	pft_grid slab_grid;
+	int slab_gls, slab_dev;
+	int device_valid;             /* slab X holds the solution left by the previous call */
+	/* host-staged path */
+	double *d_x, *d_k1, *d_k3, *d_k4, *d_k5, *d_aux, *d_eps;
+	int *d_cs, *d_cz; double * d_cm; int d_nch, d_cap;
+	double *h_k, *h_aux; int h_cap;
+	/* options */
+	int opt_gls, opt_kz, opt_dev, opt_timing;
+	pft_solver_stats stats;
+} solver_state;
+
+static __thread solver_state R = { .slab_dev = -1, .opt_kz = 16, .opt_dev = -1 };
+
+static pft_comm * comm(void)
+{
+	pft_comm * c = pft_comm_current();
+	if(c) return c;
+	if(!R.self_comm) pft_comm_init_self(&R.self_comm);
+	return R.self_comm;
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* lifecycle, hybrid2.c:72-212 */
+
+int RK_MPI_SA_init(int max_block_size, MPI_Comm comm_handle, int master_rank)
+{
+	pft_comm * c = comm();
+	(void)comm_handle;            /* the ranks are those of the pft communicator (pft_comm.h) */
+	if(!c) return -4;                                       /* :95 */
+	if(R.max_n) return -3;                                  /* :98 */
+	if(max_block_size <= 0) return -2;                      /* :99 */
+	if(master_rank < 0 || master_rank >= pft_comm_size(c)) return -4;
+	/* device buffers are sized by the path the first solve() takes (:101-112) */
+	R.max_n = max_block_size;                               /* :114-118 */
+	R.last_nan = 0;
+	R.master = master_rank;
+	return 0;
+}
+
+static void free_staged(void)
+{
+	pft_flat_free(R.d_x); pft_flat_free(R.d_k1); pft_flat_free(R.d_k3); pft_flat_free(R.d_k4);
+	pft_flat_free(R.d_k5); pft_flat_free(R.d_aux); pft_flat_free(R.d_eps);
+	pft_dev_free(R.d_cs); pft_dev_free(R.d_cz); pft_flat_free(R.d_cm);
+	R.d_x = R.d_k1 = R.d_k3 = R.d_k4 = R.d_k5 = R.d_aux = R.d_eps = R.d_cm = NULL;
+	R.d_cs = R.d_cz = NULL; R.d_cap = 0; R.d_nch = 0;
+	free(R.h_k); free(R.h_aux); R.h_k = R.h_aux = NULL; R.h_cap = 0;
+}
+
+int RK_MPI_SA_cleanup(void)
+{
+	if(R.max_n == 0) return -3;                             /* :130 */
+	if(R.slab) { pft_comm_attach(comm(), NULL); pft_slab_destroy(R.slab); R.slab = NULL; }
+	free_staged();
+	R.device_valid = 0;
+	R.max_n = 0;                                            /* :134 */
+	return 0;
+}
+
+void RK_MPI_SA_handle_NAN(int hN) { R.handle_nan = (hN == 0) ? 0 : 1; }   /* :165 */
+int RK_MPI_SA_check_NAN() { return R.last_nan; }                           /* :176 */
+
+int RK_MPI_SA_check_mem(RK_MEM_DIST * n)
+{
+	/* :191-211 */
+	int offset = 0, prev, i;
+	if(R.max_n == 0) return -3;
+	if(n->n_chunks <= 0) return -7;
+	for(i=0;i<n->n_chunks;i++) {
+		prev = offset;
+		offset = n->chunk_start[i];
+		if(offset < prev) return -6;
+		prev = offset;
+		offset += n->chunk_size[i];
+		if(offset <= prev) return -6;
+	}
+	if(offset > R.max_n) return -5;
+	return 0;
+}
+
+int pft_solver_set_option(int opt, long value)
+{
+	switch(opt) {
+		case PFT_OPT_GL_STATIC: R.opt_gls = value ? 1 : 0; return 0;
+		case PFT_OPT_KZ: if(value < 1) return -2; R.opt_kz = (int)value; if(R.slab) pft_slab_set_kz(R.slab, R.opt_kz); return 0;
+		case PFT_OPT_DEVICE: R.opt_dev = (int)value; return 0;
+		case PFT_OPT_TIMING: R.opt_timing = value ? 1 : 0; return 0;
+	}
+	return -2;
+}
+
+int pft_solver_get_stats(pft_solver_stats * st) { *st = R.stats; return 0; }
+pft_slab * pft_solver_slab(void) { return R.slab; }
+
+/* ---------------------------------------------------------------------------------------- */
+/* fused device path */
+
+static int ensure_slab(void)
+{
+	pft_grid g;
+	pft_consts c;
+	pft_slab_desc d;
+	int rc;
+	if(pft_model_get_grid(&g) || pft_model_get_consts(&c)) return -2;
+	if(R.slab && R.slab_grid.n1 == g.n1 && R.slab_grid.n2 == g.n2 && R.slab_grid.n3 == g.n3 &&
+	   R.slab_grid.rank == g.rank && R.slab_grid.nprocs == g.nprocs && R.slab_grid.calc_mode == g.calc_mode &&
+	   R.slab_gls == R.opt_gls && R.slab_dev == R.opt_dev) {
+		/* parameters may change between calls: refresh the constants */
+		pft_slab_set_consts(R.slab, &c);
+	} else if(R.slab) {
+		pft_comm_attach(comm(), NULL);
+		pft_slab_destroy(R.slab); R.slab = NULL; R.device_valid = 0;
+	}
+	if(!R.slab) {
+		if(R.opt_dev >= 0 && (rc = pft_hip_set_device(R.opt_dev))) return rc;
+		memset(&d, 0, sizeof(d));
+		d.n1 = g.n1; d.n2 = g.n2; d.n3 = g.n3;
+		d.has_below = g.rank > 0;
+		d.has_above = g.rank < g.nprocs - 1;
+		d.calc_mode = g.calc_mode;
+		d.gl_static = R.opt_gls;
+		d.eps_mult[0] = d.eps_mult[1] = d.eps_mult[2] = 1.0;
+		if((rc = pft_slab_create(&R.slab, &d, &c))) return rc;
+		pft_slab_set_kz(R.slab, R.opt_kz);
+		R.slab_grid = g; R.slab_gls = R.opt_gls; R.slab_dev = R.opt_dev;
+		R.device_valid = 0;
+	}
+	pft_comm_attach(comm(), R.slab);
+	return pft_slab_set_noise(R.slab, pft_model_noise());
+}
+
+static int canonical_chunks(const RK_MEM_DIST * n, double em[3])
+{
+	/* the intertrack chunk table (intertrack.c:2144-2157) for the configured grid */
+	pft_grid g;
+	int q, k, j, c = 0;
+	long N1, row, S;
+	if(pft_model_get_grid(&g)) return 0;
+	N1 = g.n1 + 2*PFT_BCOND_THICKNESS; row = N1*(g.n2 + 2*PFT_BCOND_THICKNESS);
+	S = row*(g.n3 + 2*PFT_BCOND_THICKNESS);
+	if(n->n_chunks != PFT_VAR_COUNT*g.n2*g.n3) return 0;
+	for(q=0;q<PFT_VAR_COUNT;q++) {
+		em[q] = n->chunk_eps_mult ? n->chunk_eps_mult[c] : 1.0;
+		for(k=0;k<g.n3;k++) for(j=0;j<g.n2;j++, c++) {
+			const long s0 = q*S + (k+PFT_BCOND_THICKNESS)*row + (long)(j+PFT_BCOND_THICKNESS)*N1 + PFT_BCOND_THICKNESS;
+			if(n->chunk_start[c] != s0 || n->chunk_size[c] != g.n1) return 0;
+			if(n->chunk_eps_mult && n->chunk_eps_mult[c] != em[q]) return 0;
+		}
+	}
+	return R.max_n >= PFT_VAR_COUNT*S;
+}
+
+static int do_stage(int stage, double ts, double coef, double h, int out_buf, int nfields, long * launches)
+{
+	pft_comm * c = comm();
+	int rc, n3;
+	if(R.opt_timing) pft_slab_timing_mark(R.slab, stage, 0);
+	if(pft_comm_size(c) == 1) {
+		(*launches)++;
+		rc = pft_slab_stage(R.slab, stage, ts, coef, h, -1, -1);
+		if(R.opt_timing) pft_slab_timing_mark(R.slab, stage, 1);
+		return rc;
+	}
+	/* boundary planes first, their exchange overlaps the interior sweep */
+	n3 = R.slab_grid.n3;
+	if((rc = pft_slab_stage(R.slab, stage, ts, coef, h, 0, 1))) return rc;
+	if(n3 > 1 && (rc = pft_slab_stage(R.slab, stage, ts, coef, h, n3-1, n3))) return rc;
+	if((rc = pft_comm_halo_start(c, out_buf, 0, nfields))) return rc;
+	if(n3 > 2 && (rc = pft_slab_stage(R.slab, stage, ts, coef, h, 1, n3-1))) return rc;
+	if(R.opt_timing) pft_slab_timing_mark(R.slab, stage, 1);
+	*launches += 3;
+	return pft_comm_halo_finish(c);
+}
+
+/* shared prologue results */
+typedef struct {
+	double final_time, t, h, h_min, delta;
+	int delta_mode, handle_nan, any_cb;
+} solve_bcast;
+
+static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast * B, int command,
+                     long max_steps_total, int flags, const double * em)
+{
+	pft_comm * c = comm();
+	const int rank = pft_comm_rank(c), nprocs = pft_comm_size(c);
+	double t = B->t, h = B->h, new_h = 0.0, h2, h3, h6, h8, eps;
+	const double final_time = B->final_time, delta = B->delta, h_min = B->h_min;
+	int nonfinite, rc, ret = 0;
+	long attempted = 0, launches = 0;
+	const int nf = R.opt_gls ? 2 : 3;     /* fields whose stage values change */
+
+	if((rc = ensure_slab())) return rc;
+	pft_slab_set_eps_mult(R.slab, em);
+	if(!(flags & PFT_SOLVE_REUSE_DEVICE) || !R.device_valid) {
+		if((rc = pft_slab_upload_host(R.slab, PFT_BUF_X, system->x))) return rc;
+		if((rc = pft_slab_upload_host(R.slab, PFT_BUF_XN, system->x))) return rc;
+		if(nprocs > 1) {
+			if((rc = pft_comm_halo(c, PFT_BUF_X, 0, 3))) return rc;
+			if((rc = pft_comm_halo(c, PFT_BUF_XN, 0, 3))) return rc;
+		}
+	}
+	R.device_valid = 0;
+	R.stats.path = 1;
+
+	while(1) {
+		h2 = h/2.0; h3 = h/3.0; h6 = h/6.0; h8 = h/8.0;                          /* :355 */
+		if((rc = pft_slab_eps_reset(R.slab))) return rc;
+		/* K1 = f(t,x); aux = x + K1 h/3 ... K5 = f(t+h, aux); error norm; x(t+h) candidate */
+		if((rc = do_stage(1, t,    h3, h, PFT_BUF_A0, nf, &launches))) return rc;    /* :373-389 */
+		if((rc = do_stage(2, t+h3, h6, h, PFT_BUF_A1, nf, &launches))) return rc;    /* :392-409 */
+		if((rc = do_stage(3, t+h3, h8, h, PFT_BUF_A0, nf, &launches))) return rc;    /* :412-429 */
+		if((rc = do_stage(4, t+h2, h,  h, PFT_BUF_A1, nf, &launches))) return rc;    /* :432-450 */
+		if((rc = do_stage(5, t+h,  h3, h, PFT_BUF_XN, nf, &launches))) return rc;    /* :453,507-524,657-668 */
+		if((rc = pft_comm_allreduce_eps(c))) return rc;                          /* :572 */
+		if((rc = pft_slab_eps_fetch(R.slab, &eps, &nonfinite))) return rc;
+		if(R.opt_timing) pft_slab_timing_collect(R.slab, R.stats.stage_ms, R.stats.stage_n);
+		system->steps_total++;                                                   /* :460 */
+		attempted++;
+		R.stats.last_eps = eps;
+
+		if(B->handle_nan && nonfinite) {                                         /* :493-503 */
+			command |= RKA_CMD_NAN;
+			if(h/(final_time-t) < 1e-11) command |= RKA_CMD_h_TOO_SMALL;
+		}
+		if(B->delta_mode == DELTA_LOCAL) eps *= fabs(h3);                        /* :578 */
+		new_h = ((eps > 0.0) ? pow((delta/eps), 0.2)*0.8 : 2.0) * h;            /* :580 */
+		if(eps < delta || fabs(h) < h_min) {                                     /* :599-611 */
+			command |= RKA_CMD_UPDATE;
+			if(fabs(final_time-(t+h)) <= fabs(new_h)) command |= RKA_CMD_NEXTFINISH;
+		}
+
+		if(command & RKA_CMD_NAN) {                                              /* :626-646 */
+			R.last_nan = 1;
+			if(command & RKA_CMD_h_TOO_SMALL) { system->t = t; ret = -4; break; }
+			h /= 10;
+			command = 0;
+		} else {
+			if(command & RKA_CMD_UPDATE) {                                       /* :651-668 */
+				t += h;
+				pft_slab_accept(R.slab);
+				system->steps++;
+				if(system->Service_Callback != NULL) {                           /* :676-685 */
+					system->t = t;
+					system->h = h;
+					if(system->Service_Callback(final_time, system)) command |= RKA_CMD_BREAK;
+				}
+				if(nprocs > 1 && B->any_cb) pft_comm_bcast(c, &command, sizeof(int), R.master);   /* :690 */
+				if(command & RKA_CMD_FINISHED) break;                            /* :695 */
+				if(command & RKA_CMD_BREAK) {                                    /* :697-705 */
+					system->t = t;
+					system->h = new_h;
+					ret = 1;
+					break;
+				}
+				f = system->meta_f();                                            /* :732 */
+				if(!pft_model_is_device_rhs(f)) { ret = -2; break; }
+			}
+			if(command & RKA_CMD_NEXTFINISH) {                                   /* :743-761 */
+				system->h = new_h;
+				h = final_time - t;
+				command = RKA_CMD_FINISHED;
+			} else {
+				command = 0;
+				h = new_h;
+			}
+		}
+		if(max_steps_total > 0 && attempted >= max_steps_total) {
+			/* extension: stop between two attempted steps; the next call continues the
+			   identical trajectory (its prologue re-derives FINISHED from t, h) */
+			system->h = h;
+			ret = 2;
+			break;
+		}
+	}
+	(void)rank;
+	if(ret != 1 && ret != -4) system->t = t;                                     /* :768 */
+	R.device_valid = 1;
+	R.stats.kernel_launches = launches;
+	R.stats.steps_total = attempted;
+	if(!(flags & PFT_SOLVE_KEEP_DEVICE)) {
+		if((rc = pft_slab_download_host(R.slab, PFT_BUF_X, system->x))) return rc;
+	}
+	return ret;
+}
+
+int pft_solver_download(RK_MPI_S_SOLUTION * system)
+{
+	if(!R.slab || !R.device_valid || !system || !system->x) return -2;
+	return pft_slab_download_host(R.slab, PFT_BUF_X, system->x);
+}
+
+int pft_solver_eval_rhs(FLOAT t, const FLOAT * w, FLOAT * dw)
+{
+	/* f(t, w, dw) on host arrays: stage w into A0, exchange its boundary planes, K into K1 */
+	pft_comm * c = comm();
+	int rc;
+	if((rc = ensure_slab())) return rc;
+	if((rc = pft_slab_upload_host(R.slab, PFT_BUF_A0, w))) return rc;
+	if(pft_comm_size(c) > 1 && (rc = pft_comm_halo(c, PFT_BUF_A0, 0, 3))) return rc;
+	if((rc = pft_slab_rhs(R.slab, PFT_BUF_A0, PFT_BUF_K1, t))) return rc;
+	return pft_slab_download_host(R.slab, PFT_BUF_K1, dw);
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* host-staged path: any right-hand side, combines on the GPU over the chunk table */
+
+static int ensure_staged(const RK_MEM_DIST * n)
+{
+	int rc;
+	if(R.d_cap < R.max_n) {
+		free_staged();
+		if((rc = pft_flat_alloc(&R.d_x, R.max_n)) || (rc = pft_flat_alloc(&R.d_k1, R.max_n)) ||
+		   (rc = pft_flat_alloc(&R.d_k3, R.max_n)) || (rc = pft_flat_alloc(&R.d_k4, R.max_n)) ||
+		   (rc = pft_flat_alloc(&R.d_k5, R.max_n)) || (rc = pft_flat_alloc(&R.d_aux, R.max_n)) ||
+		   (rc = pft_flat_alloc(&R.d_eps, 2))) return rc;
+		R.d_cap = R.max_n;
+		R.h_k = (double*)calloc(R.max_n, sizeof(double));
+		R.h_aux = (double*)calloc(R.max_n, sizeof(double));
+		if(!R.h_k || !R.h_aux) return -1;
+	}
+	if(R.d_nch < n->n_chunks) {
+		pft_dev_free(R.d_cs); pft_dev_free(R.d_cz); pft_flat_free(R.d_cm);
+		if((rc = pft_dev_alloc((void**)&R.d_cs, sizeof(int)*n->n_chunks)) ||
+		   (rc = pft_dev_alloc((void**)&R.d_cz, sizeof(int)*n->n_chunks)) ||
+		   (rc = pft_flat_alloc(&R.d_cm, n->n_chunks))) return rc;
+		R.d_nch = n->n_chunks;
+	}
+	if((rc = pft_h2d(R.d_cs, n->chunk_start, sizeof(int)*n->n_chunks, NULL))) return rc;
+	if((rc = pft_h2d(R.d_cz, n->chunk_size, sizeof(int)*n->n_chunks, NULL))) return rc;
+	if(n->chunk_eps_mult) {
+		if((rc = pft_flat_h2d(R.d_cm, n->chunk_eps_mult, n->n_chunks, NULL))) return rc;
+	} else {
+		double * ones = (double*)malloc(sizeof(double)*n->n_chunks);
+		int i;
+		for(i=0;i<n->n_chunks;i++) ones[i] = 1.0;
+		rc = pft_flat_h2d(R.d_cm, ones, n->n_chunks, NULL);
+		free(ones);
+		if(rc) return rc;
+	}
+	return pft_stream_sync(NULL);
+}
+
+static int staged_rhs(RK_RightHandSide f, double t, const double * d_in, double * host_in, double * d_out)
+{
+	int rc;
+	if(d_in) {
+		if((rc = pft_flat_d2h(host_in, d_in, R.max_n, NULL)) || (rc = pft_stream_sync(NULL))) return rc;
+	}
+	f(t, host_in, R.h_k);
+	if((rc = pft_flat_h2d(d_out, R.h_k, R.max_n, NULL))) return rc;
+	return 0;
+}
+
+static int run_staged(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast * B, int command,
+                      long max_steps_total, int flags)
+{
+	pft_comm * c = comm();
+	const int nprocs = pft_comm_size(c);
+	RK_MEM_DIST * n = system->n;
+	double * x = system->x;
+	double t = B->t, h = B->h, new_h = 0.0, h2, h3, h6, h8, eps;
+	const double final_time = B->final_time, delta = B->delta, h_min = B->h_min;
+	int rc, ret = 0, nch = n->n_chunks;
+	long attempted = 0;
+	double zero2[2] = {0.0, 0.0};
+	(void)flags;
+
+	if((rc = ensure_staged(n))) return rc;
+	if((rc = pft_flat_h2d(R.d_x, x, R.max_n, NULL))) return rc;
+	R.stats.path = 2;
+
+	while(1) {
+		long long bits[2];
+		h2 = h/2.0; h3 = h/3.0; h6 = h/6.0; h8 = h/8.0;
+		if((rc = staged_rhs(f, t, NULL, x, R.d_k1))) return rc;                                   /* :373 */
+		if((rc = pft_flat_combine(1, nch, R.d_cs, R.d_cz, R.d_cm, h3, h, R.d_x, R.d_k1, R.d_k3, R.d_k3,
+		                          R.d_k4, R.d_k5, R.d_aux, R.d_eps, NULL))) return rc;          /* :378-389 */
+		if((rc = staged_rhs(f, t+h3, R.d_aux, R.h_aux, R.d_k3))) return rc;                       /* K2 in K3, :392 */
+		if((rc = pft_flat_combine(2, nch, R.d_cs, R.d_cz, R.d_cm, h6, h, R.d_x, R.d_k1, R.d_k3, R.d_k3,
+		                          R.d_k4, R.d_k5, R.d_aux, R.d_eps, NULL))) return rc;          /* :397-409 */
+		if((rc = staged_rhs(f, t+h3, R.d_aux, R.h_aux, R.d_k3))) return rc;                       /* :412 */
+		if((rc = pft_flat_combine(3, nch, R.d_cs, R.d_cz, R.d_cm, h8, h, R.d_x, R.d_k1, R.d_k3, R.d_k3,
+		                          R.d_k4, R.d_k5, R.d_aux, R.d_eps, NULL))) return rc;          /* :417-429 */
+		if((rc = staged_rhs(f, t+h2, R.d_aux, R.h_aux, R.d_k4))) return rc;                       /* :432 */
+		if((rc = pft_flat_combine(4, nch, R.d_cs, R.d_cz, R.d_cm, h, h, R.d_x, R.d_k1, R.d_k3, R.d_k3,
+		                          R.d_k4, R.d_k5, R.d_aux, R.d_eps, NULL))) return rc;          /* :437-450 */
+		if((rc = staged_rhs(f, t+h, R.d_aux, R.h_aux, R.d_k5))) return rc;                        /* :453 */
+		if((rc = pft_flat_h2d(R.d_eps, zero2, 2, NULL))) return rc;
+		if((rc = pft_flat_combine(5, nch, R.d_cs, R.d_cz, R.d_cm, h3, h, R.d_x, R.d_k1, R.d_k3, R.d_k3,
+		                          R.d_k4, R.d_k5, R.d_aux, R.d_eps, NULL))) return rc;          /* :507-524 */
+		if((rc = pft_flat_d2h((double*)bits, R.d_eps, 2, NULL)) || (rc = pft_stream_sync(NULL))) return rc;
+		if(nprocs > 1) {
+			pft_comm_allreduce_max_i64(c, &bits[0]);                                            /* :572 */
+			bits[1] &= 0xffffffffLL;
+			pft_comm_allreduce_max_i64(c, &bits[1]);
+		}
+		memcpy(&eps, &bits[0], sizeof(double));
+		system->steps_total++;
+		attempted++;
+		R.stats.last_eps = eps;
+		if(B->handle_nan && (bits[1] & 0xffffffffLL)) {
+			command |= RKA_CMD_NAN;
+			if(h/(final_time-t) < 1e-11) command |= RKA_CMD_h_TOO_SMALL;
+		}
+		if(B->delta_mode == DELTA_LOCAL) eps *= fabs(h3);
+		new_h = ((eps > 0.0) ? pow((delta/eps), 0.2)*0.8 : 2.0) * h;
+		if(eps < delta || fabs(h) < h_min) {
+			command |= RKA_CMD_UPDATE;
+			if(fabs(final_time-(t+h)) <= fabs(new_h)) command |= RKA_CMD_NEXTFINISH;
+		}
+		if(command & RKA_CMD_NAN) {
+			R.last_nan = 1;
+			if(command & RKA_CMD_h_TOO_SMALL) { system->t = t; ret = -4; break; }
+			h /= 10;
+			command = 0;
+		} else {
+			if(command & RKA_CMD_UPDATE) {
+				t += h;
+				if((rc = pft_flat_combine(6, nch, R.d_cs, R.d_cz, R.d_cm, h3, h, R.d_x, R.d_k1, R.d_k3, R.d_k3,
+				                          R.d_k4, R.d_k5, R.d_x, R.d_eps, NULL))) return rc;    /* :657-668 */
+				/* the right-hand side of the next step reads the host x */
+				if((rc = pft_flat_d2h(x, R.d_x, R.max_n, NULL)) || (rc = pft_stream_sync(NULL))) return rc;
+				system->steps++;
+				if(system->Service_Callback != NULL) {
+					system->t = t;
+					system->h = h;
+					if(system->Service_Callback(final_time, system)) command |= RKA_CMD_BREAK;
+				}
+				if(nprocs > 1 && B->any_cb) pft_comm_bcast(c, &command, sizeof(int), R.master);
+				if(command & RKA_CMD_FINISHED) break;
+				if(command & RKA_CMD_BREAK) { system->t = t; system->h = new_h; ret = 1; break; }
+				if(system->DDLBF_Rearrange != NULL) {                                              /* :726-729 */
+					n = system->n = system->DDLBF_Rearrange(n);
+					nch = n->n_chunks;
+					if((rc = ensure_staged(n))) return rc;
+				}
+				f = system->meta_f();
+			}
+			if(command & RKA_CMD_NEXTFINISH) {
+				system->h = new_h;
+				h = final_time - t;
+				command = RKA_CMD_FINISHED;
+			} else {
+				command = 0;
+				h = new_h;
+			}
+		}
+		if(max_steps_total > 0 && attempted >= max_steps_total) { system->h = h; ret = 2; break; }
+	}
+	if(ret != 1 && ret != -4) system->t = t;
+	R.stats.steps_total = attempted;
+	R.stats.kernel_launches = 6*attempted;
+	return ret;
+}
+
+/* ---------------------------------------------------------------------------------------- */
+/* solve, hybrid2.c:215-337 prologue */
+
+int pft_solve_ex(FLOAT final_time, RK_MPI_S_SOLUTION * system, long max_steps_total, int flags)
+{
+	pft_comm * c = comm();
+	const int rank = pft_comm_rank(c);
+	int error_code = 0, command = 0;
+	long long neg;
+	RK_RightHandSide f = NULL;
+	solve_bcast B;
+	RK_MEM_DIST * n;
+
+	if(system == NULL) return -2;                                               /* :249 */
+	n = system->n;
+	if(system->meta_f != NULL) f = system->meta_f();                            /* :268 */
+	if(n == NULL || n->n_chunks <= 0) error_code = -5;                          /* :276-280 */
+	else if(n->chunk_start[n->n_chunks-1] + n->chunk_size[n->n_chunks-1] > R.max_n) error_code = -5;
+	if(R.max_n == 0) error_code = -3;                                           /* :282 */
+	if(system->x == NULL || system->meta_f == NULL) error_code = -2;            /* :284 */
+	if(rank == R.master && system->delta <= 0) error_code = -2;                 /* :286 */
+	neg = -error_code;                                                          /* :294 Allreduce(MIN) */
+	pft_comm_allreduce_max_i64(c, &neg);
+	if(error_code) return error_code;                                           /* :295 */
+	if(neg > 0) return -6;                                                      /* :299 */
+
+	R.last_nan = 0;                                                             /* :316 */
+	B.final_time = final_time; B.t = system->t; B.h = system->h;
+	B.h_min = system->h_min; B.delta = system->delta; B.delta_mode = (int)system->delta_mode;
+	B.handle_nan = R.handle_nan;
+	B.any_cb = system->Service_Callback != NULL;
+	if(rank == R.master) {                                                      /* :319-325 */
+		if((B.final_time > B.t && B.h < 0) || (B.final_time < B.t && B.h > 0)) B.h *= -1;
+		if(B.h == 0 || fabs(B.final_time - B.t) <= fabs(B.h)) {
+			B.h = B.final_time - B.t;
+			command |= RKA_CMD_FINISHED;
+		}
+	}
+	if(pft_comm_size(c) > 1) {                                                  /* :328-336 */
+		pft_comm_bcast(c, &B, sizeof(B), R.master);
+		{ long long cmd = command; pft_comm_allreduce_max_i64(c, &cmd); command = (int)cmd; }
+	}
+	R.stats.nprocs = pft_comm_size(c);
+	R.stats.rank = rank;
+
+	if(pft_model_is_device_rhs(f) && system->DDLBF_Rearrange == NULL) {
+		double em[3];
+		if(canonical_chunks(n, em)) {
+			int rc = run_fused(system, f, &B, command, max_steps_total, flags, em);
+			return rc;
+		}
+	}
+	return run_staged(system, f, &B, command, max_steps_total, flags);
+}
+
+int RK_MPI_SA_solve(FLOAT final_time, RK_MPI_S_SOLUTION * system)
+{
+	return pft_solve_ex(final_time, system, 0, 0);
+}
