@@ -38,7 +38,9 @@ HBM_PEAK_GBPS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # algorithmic HBM bytes per cell of each fused stage kernel: doubles read
 # once + written once, perfect stencil reuse.  faithful: u, p, gl all evolved by the solver;
 # gl_static: dgl == 0 exploited (PFT_OPT_GL_STATIC)
-STAGE_DOUBLES = {False: {1: 9, 2: 12, 3: 15, 4: 18, 5: 18}, True: {1: 7, 2: 9, 3: 11, 4: 13, 5: 13}}
+STAGE_DOUBLES_AUX = {False: {1: 9, 2: 12, 3: 15, 4: 18, 5: 18}, True: {1: 7, 2: 9, 3: 11, 4: 13, 5: 13}}
+# recompute path: stage s reads the arrays its input is built from, writes K_s (stage 5: x(t+h))
+STAGE_DOUBLES_RC = {False: {1: 6, 2: 9, 3: 12, 4: 12, 5: 15}, True: {1: 5, 2: 7, 3: 9, 4: 9, 5: 11}}
 SURVEY_BYTES_PER_CELL_STEP = 840   # unfused solver/RHS boundary accounting
 METRIC = "Mcells·RK-steps/s at 400³ grid, 1/2/4/8 MI355X; % HBM roofline"
 
@@ -51,15 +53,23 @@ def parse():
     ap.add_argument("--grid-nodes", type=int, default=400, help="grid_nodes of the per-GPU slab")
     ap.add_argument("--mode", type=int, default=0, help="calc_mode (0 GradP, 1 SigmaP1-P, 2 Temp)")
     ap.add_argument("--gl-static", action="store_true", help="exploit dgl == 0 (bit-identical)")
-    ap.add_argument("--kz", type=int, default=0)
+    ap.add_argument("--kz", type=int, default=0, help="planes per workgroup z-march (default 8)")
+    ap.add_argument("--tile", type=int, default=32, help="32 / 16: LDS-tiled kernel, 0: cache-based")
+    ap.add_argument("--no-recompute", action="store_true",
+                    help="materialise the reference's aux arrays between stages (72 vs 54 doubles/cell-step)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-steps", type=int, default=3, help="attempted steps of the CPU sample")
     ap.add_argument("--no-timing", action="store_true", help="no HIP-event stage timing")
+    ap.add_argument("--probe", type=int, default=0,
+                    help="after the run, launch the 8-B/lane copy probe this many times "
+                         "(rocprofv3 FETCH_SIZE/WRITE_SIZE calibration, known bytes)")
     return ap.parse_args()
 
 
 def main():
     a = parse()
+    rc_path = (not a.no_recompute) and a.tile != 0
+    STAGE_DOUBLES = STAGE_DOUBLES_RC if rc_path else STAGE_DOUBLES_AUX
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -105,7 +115,8 @@ def main():
     t0 = time.time()
     sim = P.Simulation(n1, n2, total_n3, Ls, a.mode, prm, nprocs=world, rank=rank, beads=beads,
                        tau=base["tau"], tau_min=base["tau_min"], delta=base["delta"],
-                       gl_static=a.gl_static, kz=a.kz or None)
+                       gl_static=a.gl_static, kz=a.kz or None, tile=a.tile,
+                       recompute=not a.no_recompute)
     init_s = time.time() - t0
     cells_rank = n1 * n2 * sim.grid.n3
     cells_total = n1 * n2 * total_n3
@@ -180,13 +191,27 @@ def main():
         "config": {"workload": f"{a.grid_nodes}^3 default Params per GPU: {n1}x{n2}x{n3_slab} cells/GPU, "
                                f"global {n1}x{n2}x{total_n3} (Z-slab weak scaling)",
                    "calc_mode": a.mode, "cells": cells_total, "parallelism": f"zslab{world}",
-                   "gl_static": a.gl_static, "kz": a.kz or 16,
+                   "gl_static": a.gl_static, "kz": a.kz or 8, "tile": a.tile, "recompute": not a.no_recompute,
                    "accepted_steps_total": int(sim.system.steps), "t_end": sim.t},
         "roofline": roof,
         "fused_effective_GBps": round(step_bytes * cells_total * steps / el / 1e9 / world, 1),
         "survey_840B_equiv_GBps": round(SURVEY_BYTES_PER_CELL_STEP * cells_total * steps / el / 1e9 / world, 1),
         "init_s": round(init_s, 2),
     }
+
+    if a.probe:
+        slab = L.pft_solver_slab()
+        L.pft_slab_buffer.restype = C.c_void_p
+        L.pft_slab_buffer.argtypes = [C.c_void_p, C.c_int]
+        L.pft_slab_state_bytes.restype = C.c_size_t
+        L.pft_slab_state_bytes.argtypes = [C.c_void_p]
+        L.pft_probe_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        nd = L.pft_slab_state_bytes(slab) // 8
+        src, dst = L.pft_slab_buffer(slab, 5), L.pft_slab_buffer(slab, 6)   # K3 -> K4 scratch
+        for _ in range(a.probe):
+            L.pft_probe_copy(dst, src, nd, L.pft_slab_stream(slab))
+        L.pft_hip_device_sync()
+        out["probe_bytes_each_way"] = nd * 8
 
     # ---- CPU baseline (rank 0, N = 1 only): the oracle port, bounded sample -----------------
     cpu = None

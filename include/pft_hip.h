@@ -75,6 +75,16 @@ void * pft_slab_scratch(pft_slab * s);                /* device: u64 eps bits, u
 const pft_slab_desc * pft_slab_get_desc(const pft_slab * s);
 /* planes per workgroup z-march (tuning knob, default 16) */
 int pft_slab_set_kz(pft_slab * s, int kz);
+/* stage kernel flavour: 32 (default) or 16 = LDS-tiled kernel with 64x8 / 32x16 cell tiles
+   (n1 even); 0 = cache-based kernel (any n1; also used automatically for odd n1) */
+int pft_slab_set_tile(pft_slab * s, int wx);
+/* 1 (default): the tiled kernels rebuild every stage input from x and the K's inside the
+   stencil (no aux arrays: 54 instead of 72 doubles of traffic per cell-step, bit-identical);
+   0: the reference's aux arrays are materialised between stages */
+int pft_slab_set_recompute(pft_slab * s, int on);
+/* buffer written by stage 1..5 of the step on this slab's path (its boundary planes are what
+   the z-neighbours need before the next stage) */
+int pft_slab_stage_output(const pft_slab * s, int stage);
 
 /* host layout (reference padded, ghost thickness 2) <-> device layout, on the compute stream */
 int pft_slab_upload_host(pft_slab * s, int which, const double * host_padded);
@@ -125,6 +135,8 @@ int pft_stream_sync(void * stream);
 int pft_dev_alloc(void ** p, size_t bytes);
 int pft_dev_free(void * p);
 int pft_h2d(void * dst, const void * src, size_t bytes, void * stream);
+/* diagnostic: plain 8-byte-per-lane device copy (rocprofv3 FETCH_SIZE/WRITE_SIZE calibration) */
+int pft_probe_copy(double * dst, const double * src, size_t n, void * stream);
 
 /* peer copy of one ghost plane between slabs on the same process (loopback transport) */
 int pft_memcpy_d2d_async(void * dst, const void * src, size_t bytes, void * stream);

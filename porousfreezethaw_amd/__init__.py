@@ -13,7 +13,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "lib", "libpft.so")
+LIB_PATH = os.environ.get("PFT_LIB") or os.path.join(HERE, "lib", "libpft.so")
 
 PARAM_NAMES = [  # model.c:44-59, the order of param[] (include/pft_model.h)
     "u_star", "L", "xi", "a", "b", "alpha", "mu",
@@ -27,7 +27,7 @@ BCOND_THICKNESS = 2
 DELTA_LOCAL, DELTA_GLOBAL = 0, 1
 RKA_CMD_FINISHED = 8
 PFT_SOLVE_KEEP_DEVICE, PFT_SOLVE_REUSE_DEVICE = 1, 2
-PFT_OPT_GL_STATIC, PFT_OPT_KZ, PFT_OPT_DEVICE, PFT_OPT_TIMING = 1, 2, 3, 4
+PFT_OPT_GL_STATIC, PFT_OPT_KZ, PFT_OPT_DEVICE, PFT_OPT_TIMING, PFT_OPT_TILE, PFT_OPT_RECOMPUTE = 1, 2, 3, 4, 5, 6
 MPI_COMM_WORLD = 0x44000000
 
 # every function of the public headers, for the "library exports its ABI" check
@@ -171,7 +171,7 @@ class Simulation:
 
     def __init__(self, n1, n2, total_n3, L, calc_mode, params, nprocs=1, rank=0, beads=None,
                  initial=None, tau=1.0, tau_min=0.0, delta=1e-3, t0=0.0, gl_static=False, kz=None,
-                 init_solver=True):
+                 init_solver=True, tile=None, recompute=True):
         L1, L2, L3 = L
         self.lib = L_ = lib()
         self.grid = pft_grid()
@@ -201,8 +201,9 @@ class Simulation:
         self.system = RK_MPI_S_SOLUTION(C.pointer(self.mem), t0, _dp(self.x), self.meta_addr, tau,
                                         tau_min, delta, DELTA_GLOBAL, None, None, 0, 0)
         L_.pft_solver_set_option(PFT_OPT_GL_STATIC, 1 if gl_static else 0)
-        if kz:
-            L_.pft_solver_set_option(PFT_OPT_KZ, kz)
+        L_.pft_solver_set_option(PFT_OPT_KZ, kz or 8)
+        L_.pft_solver_set_option(PFT_OPT_TILE, 32 if tile is None else tile)
+        L_.pft_solver_set_option(PFT_OPT_RECOMPUTE, 1 if recompute else 0)
         self.initialised = False
         if L_.AllocPrecalcData():
             raise RuntimeError("AllocPrecalcData failed")

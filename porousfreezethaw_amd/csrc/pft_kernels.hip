@@ -28,6 +28,12 @@
 
 #define PFT_BLOCK 256
 
+// stage 5 of the recompute kernel keeps the combine operands of planes k and k+1 in registers
+// (measured 0.52 vs 0.65 ms at 400^3: re-loading them one plane later misses the 4 MiB L2)
+#ifndef PFT_S5_RELOAD
+#define PFT_S5_KEEP 1
+#endif
+
 static __thread char g_err[256];
 
 static int fail(hipError_t e, const char* what)
@@ -68,6 +74,12 @@ __device__ __forceinline__ void rhs_cell(const pft_consts& c, const Col& u, cons
 {
   // un = u + u_noise (equation.c:676,687); only the reaction terms see the noise
   const double pc = p.c, gc = g.c, uc = u.c;
+#ifdef PFT_ABLATE_RHS
+  // diagnostic build only (never shipped): same loads and stores, trivial arithmetic
+  du = ((u.xm + u.xp) + (u.ym + u.yp)) + ((u.zm + u.zp) + un) + gc;
+  dp = ((p.xm + p.xp) + (p.ym + p.yp)) + ((p.zm + p.zp) + pc) + (g.xm + g.xp + g.ym + g.yp + g.zm + g.zp);
+  return;
+#endif
   const double rho = gc * c.rho_g + (1.0 - gc) * (pc * c.rho_i + (1.0 - pc) * c.rho_w);
   const double cp = gc * c.cp_g + (1.0 - gc) * (pc * c.cp_i + (1.0 - pc) * c.cp_w);
   const double wi = fmax(0.0, 1.0 - c.zeta * gc);
@@ -134,6 +146,9 @@ struct StageArgs {
   double T_top;        // Dirichlet value T_top(t_stage), equation.c:110
   double coef, h;
   double em0, em1, em2;
+  // recompute path (merson_fused): the stage input is rebuilt from x and the K's
+  const double* k2;    // K2 (stored only on this path; the reference aliases it with K3)
+  double cin;          // coefficient of the stage-input combine: h3, h6, h8, h for stages 2..5
 };
 
 __device__ __forceinline__ int xcd_remap(int b, int n)
@@ -193,7 +208,11 @@ __global__ __launch_bounds__(PFT_BLOCK) void merson_stage(StageArgs a, pft_const
 
   double m = 0.0;
   bool nf = false;
-  double zm[3], zc[3], zp[3];
+  // software pipeline over the z-march (the loads of plane k+1's x/y neighbours and of plane
+  // k+2's centre are in flight while plane k is computed):
+  //   zm/zc/zp: centres of planes k-1, k, k+1;  nb: x/y neighbours of plane k;
+  //   zn: centre of plane k+2 and nn: x/y neighbours of plane k+1 (prefetched)
+  double zm[3], zc[3], zp[3], zn[3], nb[3][4], nn[3][4];
   if (kb < ke) {
     const long o0 = (long)(kb + 1) * a.plane + cc;
 #pragma unroll
@@ -201,25 +220,53 @@ __global__ __launch_bounds__(PFT_BLOCK) void merson_stage(StageArgs a, pft_const
       zc[q] = fin[q][o0];
       // bottom wall: mirror (equation.c:164-174); slab interface: ghost plane
       zm[q] = (kb == 0 && !a.has_below) ? zc[q] : fin[q][o0 - a.plane];
+      zp[q] = (kb == a.n3 - 1 && !a.has_above) ? zc[q] : fin[q][o0 + a.plane];
+      nb[q][0] = fin[q][o0 + oxm];
+      nb[q][1] = fin[q][o0 + oxp];
+      nb[q][2] = fin[q][o0 + oym];
+      nb[q][3] = fin[q][o0 + oyp];
     }
   }
   for (int k = kb; k < ke; ++k) {
     const long o = (long)(k + 1) * a.plane + cc;
     const bool top = (k == a.n3 - 1) && !a.has_above;
+    // pointwise operands of this plane's stage combine, issued before the stencil arithmetic
+    double xv[3], k1v[3], k3v[3], k4v[3];
+    if (STAGE >= 1) {
 #pragma unroll
-    for (int q = 0; q < 3; ++q) zp[q] = top ? zc[q] : fin[q][o + a.plane];
-    if (top) zp[0] = a.T_top;                       // Dirichlet u (equation.c:175-183)
+      for (int q = 0; q < 3; ++q) {
+        if (GLS && q == 2) continue;
+        xv[q] = a.x[q * a.fs + o];
+        if (STAGE >= 2) k1v[q] = a.k1[q * a.fs + o];
+        if (STAGE >= 4) k3v[q] = a.k3[q * a.fs + o];
+        if (STAGE >= 5) k4v[q] = a.k4[q * a.fs + o];
+      }
+    }
+    // prefetch for the next plane
+    if (k + 1 < ke) {
+      const long o1 = o + a.plane;
+      const bool top2 = (k + 1 == a.n3 - 1) && !a.has_above;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        nn[q][0] = fin[q][o1 + oxm];
+        nn[q][1] = fin[q][o1 + oxp];
+        nn[q][2] = fin[q][o1 + oym];
+        nn[q][3] = fin[q][o1 + oyp];
+        zn[q] = top2 ? 0.0 : fin[q][o1 + a.plane];
+      }
+    }
     Col col[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       col[q].c = zc[q];
-      col[q].xm = fin[q][o + oxm];
-      col[q].xp = fin[q][o + oxp];
-      col[q].ym = fin[q][o + oym];
-      col[q].yp = fin[q][o + oyp];
+      col[q].xm = nb[q][0];
+      col[q].xp = nb[q][1];
+      col[q].ym = nb[q][2];
+      col[q].yp = nb[q][3];
       col[q].zm = zm[q];
-      col[q].zp = zp[q];
+      col[q].zp = top ? zc[q] : zp[q];               // top wall: mirror ...
     }
+    if (top) col[0].zp = a.T_top;                    // ... except Dirichlet u (equation.c:175-183)
     double du = 0.0, dp = 0.0;
     const double un = a.noise ? zc[0] + a.noise[(long)k * a.plane + cc] : zc[0];
     rhs_cell<MODE>(c, col[0], col[1], col[2], un, du, dp);
@@ -229,15 +276,39 @@ __global__ __launch_bounds__(PFT_BLOCK) void merson_stage(StageArgs a, pft_const
         a.kout[a.fs + o] = dp;
         a.kout[2 * a.fs + o] = 0.0;
       } else {
-        combine<STAGE, GLS>(a, 0, o, du, &m, nf);
-        combine<STAGE, GLS>(a, 1, o, dp, &m, nf);
-        if (!GLS) combine<STAGE, GLS>(a, 2, o, 0.0, &m, nf);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          if (GLS && q == 2) continue;
+          const double K = q == 0 ? du : (q == 1 ? dp : 0.0);   // dgl = 0 (equation.c:731)
+          const long e = q * a.fs + o;
+          if (STAGE == 1) {
+            a.kout[e] = K;
+            a.out[e] = K * a.coef + xv[q];                                         // hybrid2.c:388
+          } else if (STAGE == 2) {
+            a.out[e] = (k1v[q] + K) * a.coef + xv[q];                              // :408
+          } else if (STAGE == 3) {
+            a.kout[e] = K;
+            a.out[e] = (k1v[q] + 3.0 * K) * a.coef + xv[q];                        // :428
+          } else if (STAGE == 4) {
+            a.kout[e] = K;
+            a.out[e] = (0.5 * k1v[q] - 1.5 * k3v[q] + 2.0 * K) * a.h + xv[q];     // :449
+          } else if (STAGE == 5) {
+            const double em = q == 0 ? a.em0 : (q == 1 ? a.em1 : a.em2);
+            const double ev = em * fabs(0.2 * k1v[q] - 0.9 * k3v[q] + 0.8 * k4v[q] - 0.1 * K);  // :521
+            if (ev > m) m = ev;                                                    // :522 NaN never wins
+            nf |= !isfinite(ev);
+            a.out[e] = xv[q] + a.coef * (0.5 * (k1v[q] + K) + 2.0 * k4v[q]);      // :667
+          }
+        }
       }
     }
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       zm[q] = zc[q];
       zc[q] = zp[q];
+      zp[q] = zn[q];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) nb[q][d] = nn[q][d];
     }
   }
 
@@ -265,6 +336,440 @@ __global__ __launch_bounds__(PFT_BLOCK) void merson_stage(StageArgs a, pft_const
         bnf |= rnf[k];
       }
       // non-negative doubles order like their bit patterns
+      if (bm > 0.0) atomicMax(a.eps_bits, (unsigned long long)__double_as_longlong(bm));
+      if (bnf) atomicOr(a.nonfinite, 1u);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// the LDS-tiled fused stage kernel (n1 even): a 256-thread workgroup owns a TX x TY tile of the
+// (x, y) plane, two x-adjacent cells per thread (16-byte loads and stores everywhere), and marches
+// kz planes in z.  Plane k of the stage input sits in LDS with a halo (one row above/below, one
+// 16-byte pair left/right), so each input value is fetched from memory once per plane instead
+// of five times; plane k+1 is staged into the second LDS buffer while plane k is computed (the
+// thread's own centre values double as the z+1 neighbours, the halo ring is one 16-byte load per
+// thread).  The z-neighbours stay in registers.
+
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+template <int WX>
+struct TileGeo {
+  static constexpr int TX = 2 * WX;              // cells in x
+  static constexpr int TY = PFT_BLOCK / WX;      // rows in y
+  static constexpr int LW = TX + 4;              // LDS row: 2-cell halo each side (16-B pairs)
+  static constexpr int LH = TY + 2;              // LDS rows: 1-row halo
+  static constexpr int LF = LW * LH;             // doubles per field and plane
+  static constexpr int NH = LW + 2 * TY;         // halo pairs per field: 2 rows of LW/2, 2 per inner row
+};
+
+__device__ __forceinline__ dbl2 ld2(const double* p) { return *reinterpret_cast<const dbl2*>(p); }
+__device__ __forceinline__ void st2(double* p, dbl2 v) { *reinterpret_cast<dbl2*>(p) = v; }
+
+template <int STAGE, int MODE, bool GLS, int WX>
+__global__ __launch_bounds__(PFT_BLOCK) void merson_tile(StageArgs a, pft_consts c)
+{
+  using G = TileGeo<WX>;
+  __shared__ __attribute__((aligned(16))) double lds[2][3][G::LF];
+
+  const int ntx = (a.n1 + G::TX - 1) / G::TX;
+  const int lin = xcd_remap(blockIdx.x, a.ntile * a.nchunk);
+  const int tile = lin % a.ntile, chunk = lin / a.ntile;
+  const int x0 = (tile % ntx) * G::TX, y0 = (tile / ntx) * G::TY;
+  const int tx = threadIdx.x % WX, ty = threadIdx.x / WX;
+  const int i0 = x0 + 2 * tx, j = y0 + ty;
+  const bool active = (i0 < a.n1) && (j < a.n2);
+  const long po = (long)(j < a.n2 ? j : a.n2 - 1) * a.n1 + (i0 < a.n1 ? i0 : a.n1 - 2);   // own pair
+  const int kb = a.k_begin + chunk * a.kz;
+  const int ke = min(kb + a.kz, a.k_end);
+  const int lo = (ty + 1) * G::LW + 2 + 2 * tx;                                            // own pair in LDS
+
+  // halo pair served by this thread (field hf, LDS index hl, plane offset hp)
+  const int t = threadIdx.x;
+  const bool hact = t < 3 * G::NH;
+  const int hf = hact ? t / G::NH : 0, h = hact ? t % G::NH : 0;
+  int hr, hcp;
+  if (h < G::LW / 2) { hr = 0; hcp = h; }
+  else if (h < G::LW) { hr = G::LH - 1; hcp = h - G::LW / 2; }
+  else { const int q = h - G::LW; hr = 1 + q / 2; hcp = (q & 1) ? G::LW / 2 - 1 : 0; }
+  const int hi = x0 - 2 + 2 * hcp, hj = y0 + hr - 1;
+  const bool hin = hi >= 0 && hi < a.n1 && hj >= 0 && hj < a.n2;
+  const long hp = hin ? (long)hj * a.n1 + hi : po;        // out of the domain: never read (walls)
+  const int hl = hr * G::LW + 2 * hcp;
+
+  const double* fin[3] = {a.in, a.in + a.fs, GLS ? a.x + 2 * a.fs : a.in + 2 * a.fs};
+  const double* hsrc = fin[hf] + hp;
+
+  double m = 0.0;
+  bool nf = false;
+  dbl2 zm[3], zc[3], zp[3], zn[3];
+  int cur = 0;
+  if (kb < ke) {
+    const long o0 = (long)(kb + 1) * a.plane + po;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      zc[q] = ld2(fin[q] + o0);
+      zm[q] = (kb == 0 && !a.has_below) ? zc[q] : ld2(fin[q] + o0 - a.plane);
+      zp[q] = (kb == a.n3 - 1 && !a.has_above) ? zc[q] : ld2(fin[q] + o0 + a.plane);
+      st2(&lds[0][q][lo], zc[q]);
+    }
+    if (hact) st2(&lds[0][hf][hl], ld2(hsrc + (long)(kb + 1) * a.plane));
+    __syncthreads();
+  }
+  for (int k = kb; k < ke; ++k) {
+    const long o = (long)(k + 1) * a.plane + po;
+    const bool top = (k == a.n3 - 1) && !a.has_above;
+    const bool more = k + 1 < ke;
+    // pointwise operands of this plane's combine
+    dbl2 xv[3], k1v[3], k3v[3], k4v[3];
+    if (STAGE >= 1) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        if (GLS && q == 2) continue;
+        xv[q] = ld2(a.x + q * a.fs + o);
+        if (STAGE >= 2) k1v[q] = ld2(a.k1 + q * a.fs + o);
+        if (STAGE >= 4) k3v[q] = ld2(a.k3 + q * a.fs + o);
+        if (STAGE >= 5) k4v[q] = ld2(a.k4 + q * a.fs + o);
+      }
+    }
+    // stage plane k+1 into the other buffer: own centres now, the halo ring after the arithmetic
+    dbl2 hv = {0.0, 0.0};
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        zn[q] = ld2(fin[q] + o + 2 * (long)a.plane);
+        st2(&lds[cur ^ 1][q][lo], zp[q]);
+      }
+      if (hact) hv = ld2(hsrc + (long)(k + 2) * a.plane);
+    }
+    double du[2], dp[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      Col col[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const double* L = lds[cur][q];
+        const double cen = zc[q][s];
+        col[q].c = cen;
+        if (s == 0) {
+          col[q].xm = i0 > 0 ? L[lo - 1] : cen;
+          col[q].xp = zc[q][1];
+        } else {
+          col[q].xm = zc[q][0];
+          col[q].xp = i0 + 2 < a.n1 ? L[lo + 2] : cen;
+        }
+        col[q].ym = j > 0 ? L[lo - G::LW + s] : cen;
+        col[q].yp = j < a.n2 - 1 ? L[lo + G::LW + s] : cen;
+        col[q].zm = zm[q][s];
+        col[q].zp = top ? cen : zp[q][s];
+      }
+      if (top) col[0].zp = a.T_top;
+      const double un = a.noise ? zc[0][s] + a.noise[(long)k * a.plane + po + s] : zc[0][s];
+      rhs_cell<MODE>(c, col[0], col[1], col[2], un, du[s], dp[s]);
+    }
+    if (more && hact) st2(&lds[cur ^ 1][hf][hl], hv);
+    if (active) {
+      if (STAGE == 0) {
+        st2(a.kout + o, dbl2{du[0], du[1]});
+        st2(a.kout + a.fs + o, dbl2{dp[0], dp[1]});
+        st2(a.kout + 2 * a.fs + o, dbl2{0.0, 0.0});
+      } else {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          if (GLS && q == 2) continue;
+          const dbl2 K = q == 0 ? dbl2{du[0], du[1]} : (q == 1 ? dbl2{dp[0], dp[1]} : dbl2{0.0, 0.0});
+          const long e = q * a.fs + o;
+          dbl2 r;
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            if (STAGE == 1) r[s] = K[s] * a.coef + xv[q][s];                                   // hybrid2.c:388
+            else if (STAGE == 2) r[s] = (k1v[q][s] + K[s]) * a.coef + xv[q][s];                 // :408
+            else if (STAGE == 3) r[s] = (k1v[q][s] + 3.0 * K[s]) * a.coef + xv[q][s];           // :428
+            else if (STAGE == 4) r[s] = (0.5 * k1v[q][s] - 1.5 * k3v[q][s] + 2.0 * K[s]) * a.h + xv[q][s];  // :449
+            else {
+              const double em = q == 0 ? a.em0 : (q == 1 ? a.em1 : a.em2);
+              const double ev = em * fabs(0.2 * k1v[q][s] - 0.9 * k3v[q][s] + 0.8 * k4v[q][s] - 0.1 * K[s]);  // :521
+              if (ev > m) m = ev;                                                               // NaN never wins
+              nf |= !isfinite(ev);
+              r[s] = xv[q][s] + a.coef * (0.5 * (k1v[q][s] + K[s]) + 2.0 * k4v[q][s]);          // :667
+            }
+          }
+          if (STAGE == 1 || STAGE == 3 || STAGE == 4) st2(a.kout + e, K);
+          st2(a.out + e, r);
+        }
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      zm[q] = zc[q];
+      zc[q] = zp[q];
+      zp[q] = zn[q];
+    }
+  }
+
+  if (STAGE == 5) {
+    __shared__ double red[PFT_BLOCK / 64];
+    __shared__ int rnf[PFT_BLOCK / 64];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double ov = __shfl_xor(m, off, 64);
+      if (ov > m) m = ov;
+    }
+    const int anynf = __any(nf);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+      red[w] = m;
+      rnf[w] = anynf;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double bm = red[0];
+      int bnf = rnf[0];
+      for (int q = 1; q < PFT_BLOCK / 64; ++q) {
+        if (red[q] > bm) bm = red[q];
+        bnf |= rnf[q];
+      }
+      if (bm > 0.0) atomicMax(a.eps_bits, (unsigned long long)__double_as_longlong(bm));
+      if (bnf) atomicOr(a.nonfinite, 1u);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// the recompute kernel (default): like merson_tile, but no stage-input ("aux") array exists.
+// The reference writes aux = combine(x, K...) after each stage and the next RHS reads it
+// (hybrid2.c:378-450); here each stage kernel reads x and the K's its input is made of and
+// evaluates the same combine, with the same operands in the same order, while staging the plane
+// into LDS -- bit-identical inputs, and per cell-step 54 instead of 72 doubles of HBM traffic
+// (SURVEY 8(d)'s "fused lower bound", 432 B).  Stage s writes only K_s (stage 5: x(t+h)).
+
+struct Ops {             // operands of one 16-byte cell pair of one field
+  dbl2 x, k1, k2, k3, k4;
+};
+
+template <int STAGE, bool GLS>
+__device__ __forceinline__ void load_ops(const StageArgs& a, int q, long o, Ops& r)
+{
+  r.x = ld2(a.x + q * a.fs + o);
+  if (GLS && q == 2) return;                     // dgl == 0: the gl input is x (F4)
+  if (STAGE >= 2) r.k1 = ld2(a.k1 + q * a.fs + o);
+  if (STAGE == 3) r.k2 = ld2(a.k2 + q * a.fs + o);
+  if (STAGE >= 4) r.k3 = ld2(a.k3 + q * a.fs + o);
+  if (STAGE == 5) r.k4 = ld2(a.k4 + q * a.fs + o);
+}
+
+template <int STAGE, bool GLS>
+__device__ __forceinline__ dbl2 stage_in(const StageArgs& a, int q, const Ops& r)
+{
+  if (STAGE <= 1 || (GLS && q == 2)) return r.x;
+  dbl2 v;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    if (STAGE == 2) v[s] = r.k1[s] * a.cin + r.x[s];                                      // hybrid2.c:388
+    if (STAGE == 3) v[s] = (r.k1[s] + r.k2[s]) * a.cin + r.x[s];                          // :408
+    if (STAGE == 4) v[s] = (r.k1[s] + 3.0 * r.k3[s]) * a.cin + r.x[s];                    // :428
+    if (STAGE == 5) v[s] = (0.5 * r.k1[s] - 1.5 * r.k3[s] + 2.0 * r.k4[s]) * a.cin + r.x[s];  // :449
+  }
+  return v;
+}
+
+template <bool GLS>
+__device__ __forceinline__ void keep5(int q, const Ops& r, dbl2& x, dbl2& k1, dbl2& k4, dbl2& E)
+{
+  x = r.x;
+  if (GLS && q == 2) return;
+  k1 = r.k1;
+  k4 = r.k4;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) E[s] = 0.2 * r.k1[s] - 0.9 * r.k3[s] + 0.8 * r.k4[s];   // hybrid2.c:521 prefix
+}
+
+template <int STAGE, int MODE, bool GLS, int WX>
+__global__ __launch_bounds__(PFT_BLOCK) void merson_fused(StageArgs a, pft_consts c)
+{
+  using G = TileGeo<WX>;
+  __shared__ __attribute__((aligned(16))) double lds[2][3][G::LF];
+
+  const int ntx = (a.n1 + G::TX - 1) / G::TX;
+  const int lin = xcd_remap(blockIdx.x, a.ntile * a.nchunk);
+  const int tile = lin % a.ntile, chunk = lin / a.ntile;
+  const int x0 = (tile % ntx) * G::TX, y0 = (tile / ntx) * G::TY;
+  const int tx = threadIdx.x % WX, ty = threadIdx.x / WX;
+  const int i0 = x0 + 2 * tx, j = y0 + ty;
+  const bool active = (i0 < a.n1) && (j < a.n2);
+  const long po = (long)(j < a.n2 ? j : a.n2 - 1) * a.n1 + (i0 < a.n1 ? i0 : a.n1 - 2);
+  const int kb = a.k_begin + chunk * a.kz;
+  const int ke = min(kb + a.kz, a.k_end);
+  const int lo = (ty + 1) * G::LW + 2 + 2 * tx;
+
+  const int t = threadIdx.x;
+  const bool hact = t < 3 * G::NH;
+  const int hf = hact ? t / G::NH : 0, h = hact ? t % G::NH : 0;
+  int hr, hcp;
+  if (h < G::LW / 2) { hr = 0; hcp = h; }
+  else if (h < G::LW) { hr = G::LH - 1; hcp = h - G::LW / 2; }
+  else { const int q = h - G::LW; hr = 1 + q / 2; hcp = (q & 1) ? G::LW / 2 - 1 : 0; }
+  const int hi = x0 - 2 + 2 * hcp, hj = y0 + hr - 1;
+  const bool hin = hi >= 0 && hi < a.n1 && hj >= 0 && hj < a.n2;
+  const long hp = hin ? (long)hj * a.n1 + hi : po;
+  const int hl = hr * G::LW + 2 * hcp;
+
+  double m = 0.0;
+  bool nf = false;
+  dbl2 zm[3], zc[3], zp[3];
+#ifdef PFT_S5_KEEP
+  // stage 5 keeps x, K1, K4 and the K1/K3/K4 part of the error norm of planes k and k+1
+  dbl2 cx[3], ck1[3], ck4[3], cE[3], nx[3], nk1[3], nk4[3], nE[3];
+#endif
+  int cur = 0;
+  if (kb < ke) {
+    const long o0 = (long)(kb + 1) * a.plane + po;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      Ops cop;
+      load_ops<STAGE, GLS>(a, q, o0, cop);
+      zc[q] = stage_in<STAGE, GLS>(a, q, cop);
+#ifdef PFT_S5_KEEP
+      if (STAGE == 5) keep5<GLS>(q, cop, cx[q], ck1[q], ck4[q], cE[q]);
+#endif
+      if (kb == 0 && !a.has_below) {
+        zm[q] = zc[q];                                  // bottom wall mirror (equation.c:164-174)
+      } else {
+        Ops tmp;
+        load_ops<STAGE, GLS>(a, q, o0 - a.plane, tmp);  // plane below (exchanged ghost at kb == 0)
+        zm[q] = stage_in<STAGE, GLS>(a, q, tmp);
+      }
+      st2(&lds[0][q][lo], zc[q]);
+    }
+    if (hact) {
+      Ops tmp;
+      load_ops<STAGE, GLS>(a, hf, (long)(kb + 1) * a.plane + hp, tmp);
+      st2(&lds[0][hf][hl], stage_in<STAGE, GLS>(a, hf, tmp));
+    }
+    __syncthreads();
+  }
+  for (int k = kb; k < ke; ++k) {
+    const long o = (long)(k + 1) * a.plane + po;
+    const bool top = (k == a.n3 - 1) && !a.has_above;
+    const bool more = k + 1 < ke;
+    // z+1 neighbours: the stage input of plane k+1 (interior, or the exchanged ghost plane)
+    if (!top) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        Ops nop;
+        load_ops<STAGE, GLS>(a, q, o + a.plane, nop);
+        zp[q] = stage_in<STAGE, GLS>(a, q, nop);
+#ifdef PFT_S5_KEEP
+        if (STAGE == 5) keep5<GLS>(q, nop, nx[q], nk1[q], nk4[q], nE[q]);
+#endif
+      }
+    }
+    dbl2 hv = {0.0, 0.0};
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) st2(&lds[cur ^ 1][q][lo], zp[q]);
+      if (hact) {
+        Ops tmp;
+        load_ops<STAGE, GLS>(a, hf, (long)(k + 2) * a.plane + hp, tmp);
+        hv = stage_in<STAGE, GLS>(a, hf, tmp);
+      }
+    }
+    double du[2], dp[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      Col col[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const double* L = lds[cur][q];
+        const double cen = zc[q][s];
+        col[q].c = cen;
+        if (s == 0) {
+          col[q].xm = i0 > 0 ? L[lo - 1] : cen;
+          col[q].xp = zc[q][1];
+        } else {
+          col[q].xm = zc[q][0];
+          col[q].xp = i0 + 2 < a.n1 ? L[lo + 2] : cen;
+        }
+        col[q].ym = j > 0 ? L[lo - G::LW + s] : cen;
+        col[q].yp = j < a.n2 - 1 ? L[lo + G::LW + s] : cen;
+        col[q].zm = zm[q][s];
+        col[q].zp = top ? cen : zp[q][s];
+      }
+      if (top) col[0].zp = a.T_top;
+      const double un = a.noise ? zc[0][s] + a.noise[(long)k * a.plane + po + s] : zc[0][s];
+      rhs_cell<MODE>(c, col[0], col[1], col[2], un, du[s], dp[s]);
+    }
+    if (more && hact) st2(&lds[cur ^ 1][hf][hl], hv);
+    if (active) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        if (GLS && q == 2 && STAGE != 0) continue;
+        const dbl2 K = q == 0 ? dbl2{du[0], du[1]} : (q == 1 ? dbl2{dp[0], dp[1]} : dbl2{0.0, 0.0});
+        const long e = q * a.fs + o;
+        if (STAGE <= 4) {
+          st2(a.kout + e, K);
+        } else {
+          // operands of plane k again (loaded one iteration ago: an L2 hit; keeping them in
+          // registers as well would double the stage-5 register file and halve occupancy)
+#ifdef PFT_S5_KEEP
+          const dbl2 ox = cx[q], ok1 = ck1[q], ok4 = ck4[q], oE = cE[q];
+#else
+          Ops op;
+          load_ops<STAGE, GLS>(a, q, o, op);
+          const dbl2 ox = op.x, ok1 = op.k1, ok4 = op.k4;
+          dbl2 oE;
+#pragma unroll
+          for (int s = 0; s < 2; ++s) oE[s] = 0.2 * op.k1[s] - 0.9 * op.k3[s] + 0.8 * op.k4[s];
+#endif
+          dbl2 r;
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const double em = q == 0 ? a.em0 : (q == 1 ? a.em1 : a.em2);
+            const double ev = em * fabs(oE[s] - 0.1 * K[s]);                                    // :521
+            if (ev > m) m = ev;                                                               // NaN never wins
+            nf |= !isfinite(ev);
+            r[s] = ox[s] + a.coef * (0.5 * (ok1[s] + K[s]) + 2.0 * ok4[s]);                  // :667
+          }
+          st2(a.out + e, r);
+        }
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      zm[q] = zc[q];
+      zc[q] = zp[q];
+#ifdef PFT_S5_KEEP
+      if (STAGE == 5) { cx[q] = nx[q]; ck1[q] = nk1[q]; ck4[q] = nk4[q]; cE[q] = nE[q]; }
+#endif
+    }
+  }
+
+  if (STAGE == 5) {
+    __shared__ double red[PFT_BLOCK / 64];
+    __shared__ int rnf[PFT_BLOCK / 64];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double ov = __shfl_xor(m, off, 64);
+      if (ov > m) m = ov;
+    }
+    const int anynf = __any(nf);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+      red[w] = m;
+      rnf[w] = anynf;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double bm = red[0];
+      int bnf = rnf[0];
+      for (int q = 1; q < PFT_BLOCK / 64; ++q) {
+        if (red[q] > bm) bm = red[q];
+        bnf |= rnf[q];
+      }
       if (bm > 0.0) atomicMax(a.eps_bits, (unsigned long long)__double_as_longlong(bm));
       if (bnf) atomicOr(a.nonfinite, 1u);
     }
@@ -367,6 +872,16 @@ __global__ void flat_combine_kernel(int stage, int n_chunks, const int* __restri
 }
 
 // ------------------------------------------------------------------------------------------
+// calibration probe: a plain 8-byte-per-lane copy with a known byte count, used to calibrate
+// rocprofv3's FETCH_SIZE / WRITE_SIZE for the access width the stage kernels use
+
+__global__ void probe_copy_kernel(double* __restrict__ dst, const double* __restrict__ src, long n)
+{
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x)
+    dst[e] = src[e];
+}
+
+// ------------------------------------------------------------------------------------------
 // slab object + shim
 
 struct pft_slab {
@@ -382,6 +897,9 @@ struct pft_slab {
   hipStream_t stream, comm;
   int kz;
   double* noise;         // device u_noise (n3*plane) or null
+  int tile_wx;           // 32 / 16: LDS-tiled kernels with that many threads per row; 0: cache-based
+  int n1_tiled_ok;
+  int recompute;         // 1: stage inputs rebuilt from x and the K's (no aux arrays)
   hipEvent_t tev[6][2];  // per-stage timing events
   int tpending[6];
 };
@@ -423,7 +941,10 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
   const long raw = (long)(d->n3 + 2) * s->plane;
   s->fs = (raw + 63) & ~63L;  // 512-byte aligned field starts
   s->S = (long)(d->n1 + 4) * (d->n2 + 4) * (d->n3 + 4);
-  s->kz = 16;
+  s->kz = 8;
+  s->tile_wx = 32;
+  s->n1_tiled_ok = 1;
+  s->recompute = 1;
   const size_t bytes = sizeof(double) * 3 * (size_t)s->fs;
   for (int b = 0; b < PFT_BUF_COUNT; ++b) {
     hipError_t e = hipMalloc((void**)&s->buf[b], bytes);
@@ -476,6 +997,13 @@ size_t pft_slab_plane(const pft_slab* s) { return (size_t)s->plane; }
 int pft_slab_nz(const pft_slab* s) { return s->d.n3; }
 void* pft_slab_scratch(pft_slab* s) { return (void*)s->scratch; }
 const pft_slab_desc* pft_slab_get_desc(const pft_slab* s) { return &s->d; }
+int pft_slab_set_tile(pft_slab* s, int wx)
+{
+  if (wx != 0 && wx != 16 && wx != 32) return -2;
+  s->tile_wx = wx;
+  return 0;
+}
+
 int pft_slab_set_kz(pft_slab* s, int kz)
 {
   if (kz < 1) return -2;
@@ -519,35 +1047,74 @@ int pft_slab_download_host(pft_slab* s, int which, double* host_padded)
 
 }  // extern "C"
 
+// kernel flavours: KCACHE (any n1, aux arrays), KTILE (LDS tile, aux arrays), KFUSED (LDS tile,
+// stage inputs recomputed from x and the K's -- the default for even n1)
+enum { KCACHE = 0, KTILE = 1, KFUSED = 2 };
+
+template <int STAGE, int MODE, bool GLS>
+static void launch_kernel(int kind, int wx, dim3 g, hipStream_t st, const StageArgs& a, const pft_consts& c)
+{
+  if (kind == KFUSED) {
+    if (wx == 16)
+      merson_fused<STAGE, MODE, GLS, 16><<<g, PFT_BLOCK, 0, st>>>(a, c);
+    else
+      merson_fused<STAGE, MODE, GLS, 32><<<g, PFT_BLOCK, 0, st>>>(a, c);
+  } else if (kind == KTILE) {
+    if (wx == 16)
+      merson_tile<STAGE, MODE, GLS, 16><<<g, PFT_BLOCK, 0, st>>>(a, c);
+    else
+      merson_tile<STAGE, MODE, GLS, 32><<<g, PFT_BLOCK, 0, st>>>(a, c);
+  } else {
+    merson_stage<STAGE, MODE, GLS><<<g, PFT_BLOCK, 0, st>>>(a, c);
+  }
+}
+
 template <int STAGE, bool GLS>
-static void launch_mode(int mode, dim3 g, hipStream_t st, const StageArgs& a, const pft_consts& c)
+static void launch_mode(int mode, int kind, int wx, dim3 g, hipStream_t st, const StageArgs& a,
+                        const pft_consts& c)
 {
   switch (mode) {
-    case 0: merson_stage<STAGE, 0, GLS><<<g, PFT_BLOCK, 0, st>>>(a, c); break;
-    case 1: merson_stage<STAGE, 1, GLS><<<g, PFT_BLOCK, 0, st>>>(a, c); break;
-    case 2: merson_stage<STAGE, 2, GLS><<<g, PFT_BLOCK, 0, st>>>(a, c); break;
-    case 10: merson_stage<STAGE, 10, GLS><<<g, PFT_BLOCK, 0, st>>>(a, c); break;
-    case 11: merson_stage<STAGE, 11, GLS><<<g, PFT_BLOCK, 0, st>>>(a, c); break;
+    case 0: launch_kernel<STAGE, 0, GLS>(kind, wx, g, st, a, c); break;
+    case 1: launch_kernel<STAGE, 1, GLS>(kind, wx, g, st, a, c); break;
+    case 2: launch_kernel<STAGE, 2, GLS>(kind, wx, g, st, a, c); break;
+    case 10: launch_kernel<STAGE, 10, GLS>(kind, wx, g, st, a, c); break;
+    case 11: launch_kernel<STAGE, 11, GLS>(kind, wx, g, st, a, c); break;
   }
 }
 
 template <bool GLS>
-static void launch_stage(int stage, int mode, dim3 g, hipStream_t st, const StageArgs& a, const pft_consts& c)
+static void launch_stage(int stage, int mode, int kind, int wx, dim3 g, hipStream_t st, const StageArgs& a,
+                         const pft_consts& c)
 {
   switch (stage) {
-    case 0: launch_mode<0, GLS>(mode, g, st, a, c); break;
-    case 1: launch_mode<1, GLS>(mode, g, st, a, c); break;
-    case 2: launch_mode<2, GLS>(mode, g, st, a, c); break;
-    case 3: launch_mode<3, GLS>(mode, g, st, a, c); break;
-    case 4: launch_mode<4, GLS>(mode, g, st, a, c); break;
-    case 5: launch_mode<5, GLS>(mode, g, st, a, c); break;
+    case 0: launch_mode<0, GLS>(mode, kind, wx, g, st, a, c); break;
+    case 1: launch_mode<1, GLS>(mode, kind, wx, g, st, a, c); break;
+    case 2: launch_mode<2, GLS>(mode, kind, wx, g, st, a, c); break;
+    case 3: launch_mode<3, GLS>(mode, kind, wx, g, st, a, c); break;
+    case 4: launch_mode<4, GLS>(mode, kind, wx, g, st, a, c); break;
+    case 5: launch_mode<5, GLS>(mode, kind, wx, g, st, a, c); break;
   }
 }
 
 extern "C" {
 
+static int slab_kind(const pft_slab* s)
+{
+  if (s->d.n1 % 2 != 0 || s->tile_wx == 0) return KCACHE;   // 16-byte rows need n1 even
+  return s->recompute ? KFUSED : KTILE;
+}
+
+int pft_slab_stage_output(const pft_slab* s, int stage)
+{
+  // the buffer each stage of the step writes (and whose boundary planes neighbours need)
+  static const int aux_out[6] = {-1, PFT_BUF_A0, PFT_BUF_A1, PFT_BUF_A0, PFT_BUF_A1, PFT_BUF_XN};
+  static const int rc_out[6] = {-1, PFT_BUF_K1, PFT_BUF_A0 /* K2 */, PFT_BUF_K3, PFT_BUF_K4, PFT_BUF_XN};
+  if (stage < 1 || stage > 5) return -2;
+  return slab_kind(s) == KFUSED ? rc_out[stage] : aux_out[stage];
+}
+
 static int run_stage(pft_slab* s, int stage, const double* in, double* kout, double* out, double t_stage,
-                     double coef, double h, int k_begin, int k_end, int gls)
+                     double coef, double h, int k_begin, int k_end, int gls, int kind)
 {
   const int mode = s->d.calc_mode;
   if (mode != 0 && mode != 1 && mode != 2 && mode != 10 && mode != 11) return -2;
@@ -559,6 +1126,7 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   a.in = in;
   a.x = s->buf[PFT_BUF_X];
   a.k1 = s->buf[PFT_BUF_K1];
+  a.k2 = s->buf[PFT_BUF_A0];
   a.k3 = s->buf[PFT_BUF_K3];
   a.k4 = s->buf[PFT_BUF_K4];
   a.kout = kout;
@@ -576,38 +1144,61 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   a.k_begin = k_begin;
   a.k_end = k_end;
   a.kz = s->kz;
-  a.ntile = (s->plane + PFT_BLOCK - 1) / PFT_BLOCK;
+  const int wx = kind == KCACHE ? 0 : s->tile_wx;
+  if (wx) {
+    const int TX = 2 * wx, TY = PFT_BLOCK / wx;
+    a.ntile = ((s->d.n1 + TX - 1) / TX) * ((s->d.n2 + TY - 1) / TY);
+  } else {
+    a.ntile = (s->plane + PFT_BLOCK - 1) / PFT_BLOCK;
+  }
   a.nchunk = (k_end - k_begin + a.kz - 1) / a.kz;
   a.T_top = t_stage < s->c.phase_switch_time ? s->c.top_temp1 : s->c.top_temp2;
   a.coef = coef;
   a.h = h;
+  // stage-input coefficients of the recompute path: exactly the solver's h/3.0, h/6.0, h/8.0, h
+  a.cin = stage == 2 ? h / 3.0 : stage == 3 ? h / 6.0 : stage == 4 ? h / 8.0 : h;
+  if (kind == KFUSED && stage == 0) a.x = in;       // pure RHS: the input is the given buffer
   a.em0 = s->d.eps_mult[0];
   a.em1 = s->d.eps_mult[1];
   a.em2 = s->d.eps_mult[2];
   dim3 g((unsigned)(a.ntile * a.nchunk));
   if (gls)
-    launch_stage<true>(stage, mode, g, s->stream, a, s->c);
+    launch_stage<true>(stage, mode, kind, wx, g, s->stream, a, s->c);
   else
-    launch_stage<false>(stage, mode, g, s->stream, a, s->c);
+    launch_stage<false>(stage, mode, kind, wx, g, s->stream, a, s->c);
   HIPCHK(hipGetLastError());
   return 0;
 }
 
 int pft_slab_stage(pft_slab* s, int stage, double t_stage, double coef, double h, int k_begin, int k_end)
 {
-  // buffer rotation of the fused step: in -> (kout, out)
+  if (stage < 1 || stage > 5) return -2;
+  const int kind = slab_kind(s);
+  if (kind == KFUSED) {
+    // inputs rebuilt from x, K1, K2 (in A0), K3, K4; outputs K_stage or x(t+h)
+    static const int k_of[6] = {-1, PFT_BUF_K1, PFT_BUF_A0, PFT_BUF_K3, PFT_BUF_K4, -1};
+    return run_stage(s, stage, nullptr, k_of[stage] >= 0 ? s->buf[k_of[stage]] : nullptr,
+                     stage == 5 ? s->buf[PFT_BUF_XN] : nullptr, t_stage, coef, h, k_begin, k_end,
+                     s->d.gl_static, kind);
+  }
+  // aux path: in -> (kout, out)
   static const int in_of[6] = {-1, PFT_BUF_X, PFT_BUF_A0, PFT_BUF_A1, PFT_BUF_A0, PFT_BUF_A1};
   static const int out_of[6] = {-1, PFT_BUF_A0, PFT_BUF_A1, PFT_BUF_A0, PFT_BUF_A1, PFT_BUF_XN};
   static const int k_of[6] = {-1, PFT_BUF_K1, -1, PFT_BUF_K3, PFT_BUF_K4, -1};
-  if (stage < 1 || stage > 5) return -2;
   return run_stage(s, stage, s->buf[in_of[stage]], k_of[stage] >= 0 ? s->buf[k_of[stage]] : nullptr,
-                   s->buf[out_of[stage]], t_stage, coef, h, k_begin, k_end, s->d.gl_static);
+                   s->buf[out_of[stage]], t_stage, coef, h, k_begin, k_end, s->d.gl_static, kind);
 }
 
 int pft_slab_rhs(pft_slab* s, int in_buf, int out_buf, double t)
 {
   if (in_buf < 0 || in_buf >= PFT_BUF_COUNT || out_buf < 0 || out_buf >= PFT_BUF_COUNT) return -2;
-  return run_stage(s, 0, s->buf[in_buf], s->buf[out_buf], nullptr, t, 0.0, 0.0, -1, -1, 0);
+  return run_stage(s, 0, s->buf[in_buf], s->buf[out_buf], nullptr, t, 0.0, 0.0, -1, -1, 0, slab_kind(s));
+}
+
+int pft_slab_set_recompute(pft_slab* s, int on)
+{
+  s->recompute = on ? 1 : 0;
+  return 0;
 }
 
 int pft_slab_set_consts(pft_slab* s, const pft_consts* c)
@@ -724,6 +1315,13 @@ int pft_stream_sync(void* stream)
   HIPCHK(hipStreamSynchronize((hipStream_t)stream));
   return 0;
 }
+int pft_probe_copy(double* dst, const double* src, size_t n, void* stream)
+{
+  probe_copy_kernel<<<4096, 256, 0, (hipStream_t)stream>>>(dst, src, (long)n);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 int pft_dev_alloc(void** p, size_t bytes)
 {
   HIPCHK(hipMalloc(p, bytes));

@@ -40,11 +40,11 @@ typedef struct {
 	int *d_cs, *d_cz; double * d_cm; int d_nch, d_cap;
 	double *h_k, *h_aux; int h_cap;
 	/* options */
-	int opt_gls, opt_kz, opt_dev, opt_timing;
+	int opt_gls, opt_kz, opt_dev, opt_timing, opt_tile, opt_norecompute;
 	pft_solver_stats stats;
 } solver_state;
 
-static __thread solver_state R = { .slab_dev = -1, .opt_kz = 16, .opt_dev = -1 };
+static __thread solver_state R = { .slab_dev = -1, .opt_kz = 8, .opt_dev = -1, .opt_tile = 32 };
 
 static pft_comm * comm(void)
 {
@@ -120,6 +120,11 @@ int pft_solver_set_option(int opt, long value)
 		case PFT_OPT_KZ: if(value < 1) return -2; R.opt_kz = (int)value; if(R.slab) pft_slab_set_kz(R.slab, R.opt_kz); return 0;
 		case PFT_OPT_DEVICE: R.opt_dev = (int)value; return 0;
 		case PFT_OPT_TIMING: R.opt_timing = value ? 1 : 0; return 0;
+		case PFT_OPT_RECOMPUTE:
+			R.opt_norecompute = value ? 0 : 1; if(R.slab) pft_slab_set_recompute(R.slab, !R.opt_norecompute); return 0;
+		case PFT_OPT_TILE:
+			if(value != 0 && value != 16 && value != 32) return -2;
+			R.opt_tile = (int)value; if(R.slab) pft_slab_set_tile(R.slab, R.opt_tile); return 0;
 	}
 	return -2;
 }
@@ -157,6 +162,8 @@ static int ensure_slab(void)
 		d.eps_mult[0] = d.eps_mult[1] = d.eps_mult[2] = 1.0;
 		if((rc = pft_slab_create(&R.slab, &d, &c))) return rc;
 		pft_slab_set_kz(R.slab, R.opt_kz);
+		pft_slab_set_tile(R.slab, R.opt_tile);
+		pft_slab_set_recompute(R.slab, !R.opt_norecompute);
 		R.slab_grid = g; R.slab_gls = R.opt_gls; R.slab_dev = R.opt_dev;
 		R.device_valid = 0;
 	}
@@ -185,9 +192,10 @@ static int canonical_chunks(const RK_MEM_DIST * n, double em[3])
 	return R.max_n >= PFT_VAR_COUNT*S;
 }
 
-static int do_stage(int stage, double ts, double coef, double h, int out_buf, int nfields, long * launches)
+static int do_stage(int stage, double ts, double coef, double h, int nfields, long * launches)
 {
 	pft_comm * c = comm();
+	const int out_buf = pft_slab_stage_output(R.slab, stage);
 	int rc, n3;
 	if(R.opt_timing) pft_slab_timing_mark(R.slab, stage, 0);
 	if(pft_comm_size(c) == 1) {
@@ -241,11 +249,11 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 		h2 = h/2.0; h3 = h/3.0; h6 = h/6.0; h8 = h/8.0;                          /* :355 */
 		if((rc = pft_slab_eps_reset(R.slab))) return rc;
 		/* K1 = f(t,x); aux = x + K1 h/3 ... K5 = f(t+h, aux); error norm; x(t+h) candidate */
-		if((rc = do_stage(1, t,    h3, h, PFT_BUF_A0, nf, &launches))) return rc;    /* :373-389 */
-		if((rc = do_stage(2, t+h3, h6, h, PFT_BUF_A1, nf, &launches))) return rc;    /* :392-409 */
-		if((rc = do_stage(3, t+h3, h8, h, PFT_BUF_A0, nf, &launches))) return rc;    /* :412-429 */
-		if((rc = do_stage(4, t+h2, h,  h, PFT_BUF_A1, nf, &launches))) return rc;    /* :432-450 */
-		if((rc = do_stage(5, t+h,  h3, h, PFT_BUF_XN, nf, &launches))) return rc;    /* :453,507-524,657-668 */
+		if((rc = do_stage(1, t,    h3, h, nf, &launches))) return rc;    /* :373-389 */
+		if((rc = do_stage(2, t+h3, h6, h, nf, &launches))) return rc;    /* :392-409 */
+		if((rc = do_stage(3, t+h3, h8, h, nf, &launches))) return rc;    /* :412-429 */
+		if((rc = do_stage(4, t+h2, h,  h, nf, &launches))) return rc;    /* :432-450 */
+		if((rc = do_stage(5, t+h,  h3, h, nf, &launches))) return rc;    /* :453,507-524,657-668 */
 		if((rc = pft_comm_allreduce_eps(c))) return rc;                          /* :572 */
 		if((rc = pft_slab_eps_fetch(R.slab, &eps, &nonfinite))) return rc;
 		if(R.opt_timing) pft_slab_timing_collect(R.slab, R.stats.stage_ms, R.stats.stage_n);

@@ -1,0 +1,21 @@
+#!/bin/bash
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out/fsweep
+FLAVS=${FLAVS:-"32:rc 16:rc 32:aux"}
+for cfg in $FLAVS; do
+  tile=${cfg%%:*}; kind=${cfg##*:}
+  extra=""; [ "$kind" = "aux" ] && extra="--no-recompute"
+  for kz in ${KZS:-8 16}; do
+    for gls in "" "--gl-static"; do
+      timeout -k 10 300 python bench.py --steps 60 --warmup 5 --no-cpu --kz $kz --tile $tile $extra $gls > gpurun_out/fsweep/t${tile}${kind}_kz${kz}${gls}.json 2>>gpurun_out/fsweep/err.log
+      rc=$?; [ $rc -ge 124 ] && exit $rc
+    done
+  done
+done
+python3 - <<'PY'
+import glob, json
+for f in sorted(glob.glob("gpurun_out/fsweep/t*.json")):
+    try: d = json.load(open(f))
+    except Exception as e: print(f, "ERR", e); continue
+    print(f.split("/")[-1], d["value"], d["ms_per_step"], d["roofline"]["stages_ms"], d["fused_effective_GBps"])
+PY

@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 runs of bench.py into profiles/pmc_summary.json.
+
+Inputs (directories written by scripts/gpu_profile.sh): a kernel-trace/--stats run and two PMC
+runs (FETCH_SIZE, WRITE_SIZE -- separate passes, MI355X_MICROARCH.md "rocprofv3 PMC slots").
+Corrections (MI355X_MICROARCH.md "HBM"): FETCH_SIZE/WRITE_SIZE are in KiB; gfx950's FETCH_SIZE
+is only exact for calibrated access widths, so the ratio known/measured of the probe_copy_kernel
+(8-byte loads and stores per lane, exactly the stage kernels' width, known byte count) calibrates
+both counters.  Output keys: stage<k>_gl<0|1>_g<grid>_m<mode> -> HBM bytes per launch.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def rows(d, pattern):
+    out = []
+    for f in glob.glob(os.path.join(d, "**", pattern), recursive=True):
+        with open(f) as fh:
+            out += list(csv.DictReader(fh))
+    return out
+
+
+def counters(d, name):
+    acc = defaultdict(list)
+    for r in rows(d, "*counter_collection.csv"):
+        if r.get("Counter_Name") != name:
+            continue
+        acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def kname(k):
+    m = re.search(r"merson_stage<(\d+),\s*(\d+),\s*(true|false)>", k)
+    if m:
+        return f"stage{m.group(1)}", m.group(2), m.group(3) == "true"
+    if "probe_copy" in k:
+        return "probe", None, None
+    return None, None, None
+
+
+def main(trace_dir, fetch_dir, write_dir, grid, probe_bytes, out_path):
+    fetch, write = counters(fetch_dir, "FETCH_SIZE"), counters(write_dir, "WRITE_SIZE")
+    pf = [v for k, v in fetch.items() if kname(k)[0] == "probe"]
+    pw = [v for k, v in write.items() if kname(k)[0] == "probe"]
+    cal_f = probe_bytes / (pf[0] * 1024) if pf else 1.0
+    cal_w = probe_bytes / (pw[0] * 1024) if pw else 1.0
+    stats = {}
+    for r in rows(trace_dir, "*kernel_stats.csv"):
+        stats[r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
+                            "pct": float(r.get("Percentage", 0))}
+    res = {"calibration": {"probe_bytes": probe_bytes, "fetch_factor": cal_f, "write_factor": cal_w,
+                           "probe_FETCH_SIZE_KiB": pf[0] if pf else None,
+                           "probe_WRITE_SIZE_KiB": pw[0] if pw else None}}
+    for k in set(fetch) | set(write):
+        st, mode, gls = kname(k)
+        if not st or st == "probe":
+            continue
+        fb = fetch.get(k, 0.0) * 1024 * cal_f
+        wb = write.get(k, 0.0) * 1024 * cal_w
+        key = f"{st}_gl{int(gls)}_g{grid}_m{mode}"
+        res[key] = {"kernel": k, "fetch_bytes": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
+                    "raw_FETCH_SIZE_KiB": fetch.get(k), "raw_WRITE_SIZE_KiB": write.get(k)}
+    res["kernel_stats"] = stats
+    with open(out_path, "w") as f:
+        json.dump(res, f, indent=1, sort_keys=True)
+    print(json.dumps({k: v.get("hbm_bytes_per_launch") for k, v in res.items() if isinstance(v, dict)}, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5]), sys.argv[6])

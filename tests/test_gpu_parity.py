@@ -22,7 +22,14 @@ def need_gpu():
         pytest.fail("no HIP device: the gpu tests must run on an MI355X (no CPU fallback exists)")
 
 
-def make_sim(meta, initial, mode=None, **kw):
+# kernel flavours: (tile width, recompute stage inputs)
+FLAVOURS = {"cache": (0, False), "tile32": (32, False), "tile16": (16, False),
+            "fused32": (32, True), "fused16": (16, True)}
+
+
+def make_sim(meta, initial, mode=None, flavour=None, **kw):
+    if flavour is not None:
+        kw["tile"], kw["recompute"] = FLAVOURS[flavour]
     Pm, info = O.params_from_meta(meta)
     mode = info["calc_mode"] if mode is None else mode
     return P.Simulation(info["n1"], info["n2"], info["n3"], (info["L1"], info["L2"], info["L3"]), mode, Pm,
@@ -41,9 +48,10 @@ def assert_rhs(K, ref, mode):
 @pytest.mark.parametrize("case,key", [("g20", "ic"), ("ragged", "state")])
 @pytest.mark.parametrize("mode", [0, 1, 2, 10, 11])
 @pytest.mark.parametrize("tag", ["t0", "t1"])
-def test_rhs_device(case, key, mode, tag):
+@pytest.mark.parametrize("flavour", sorted(FLAVOURS))
+def test_rhs_device(case, key, mode, tag, flavour):
     meta, A = O.load_case(case)
-    sim, Pm, info = make_sim(meta, A[key], mode=mode, init_solver=False)
+    sim, Pm, info = make_sim(meta, A[key], mode=mode, init_solver=False, flavour=flavour)
     dw, _ = P.rhs(sim, meta["rhs_times"][tag])
     K = dw.reshape((3,) + sim.N)[:, 2:-2, 2:-2, 2:-2]
     assert_rhs(K, A[f"rhs_m{mode}_{tag}"], mode)
@@ -52,11 +60,12 @@ def test_rhs_device(case, key, mode, tag):
 
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("gl_static", [False, True])
-def test_trajectory_bitwise(mode, gl_static):
+@pytest.mark.parametrize("flavour", sorted(FLAVOURS))
+def test_trajectory_bitwise(mode, gl_static, flavour):
     """RK_MPI_SA_solve to several snapshot times (intertrack.c:2272-2283): t, h, step counts and
     the fields equal the reference's after 1171 attempted steps (mode 0)"""
     meta, A = O.load_case("g20")
-    sim, Pm, info = make_sim(meta, A[f"traj_m{mode}_ic"], mode=mode, gl_static=gl_static)
+    sim, Pm, info = make_sim(meta, A[f"traj_m{mode}_ic"], mode=mode, gl_static=gl_static, flavour=flavour)
     for i, T in enumerate(meta["traj_times"]):
         rc = sim.solve(T)
         ref = meta[f"traj_m{mode}"][i]
@@ -96,28 +105,35 @@ def test_single_step(tag):
 def test_step_limited_resident_equals_continuous():
     """pft_solve_ex in chunks of attempted steps with x kept on the device == one solve"""
     meta, A = O.load_case("g20")
-    T = meta["traj_times"][1]
     sim, Pm, info = make_sim(meta, A["traj_m0_ic"])
     flags = P.PFT_SOLVE_KEEP_DEVICE
-    while True:
-        rc = sim.solve_ex(T, 37, flags)
-        flags = P.PFT_SOLVE_KEEP_DEVICE | P.PFT_SOLVE_REUSE_DEVICE
-        if rc != 2:
-            break
+    for i, T in enumerate(meta["traj_times"][:2]):     # same snapshot times as the golden run
+        while True:
+            rc = sim.solve_ex(T, 37, flags)
+            flags = P.PFT_SOLVE_KEEP_DEVICE | P.PFT_SOLVE_REUSE_DEVICE
+            if rc != 2:
+                break
+        ref = meta["traj_m0"][i]
+        assert (sim.t, sim.system.steps, sim.system.steps_total) == (float.fromhex(ref[0]), ref[2], ref[3])
     sim.download()
-    ref = meta["traj_m0"][1]
-    assert (sim.t, sim.system.steps, sim.system.steps_total) == (float.fromhex(ref[0]), ref[2], ref[3])
     assert np.array_equal(sim.interior(), A["traj_m0_state1"])
     sim.close()
 
 
-def test_matches_oracle_larger_grid():
-    """default Params at grid_nodes 60 (30x30x60) from the default IC, 12 attempted steps"""
+@pytest.mark.parametrize("dims,flavour", [((30, 30, 60), "fused32"), ((30, 30, 60), "fused16"),
+                                          ((66, 38, 21), "fused32"), ((17, 9, 13), "fused32"),
+                                          ((130, 70, 9), "fused16"), ((66, 38, 21), "tile32"),
+                                          ((130, 70, 9), "cache")])
+def test_matches_oracle_larger_grid(dims, flavour):
+    """default Params on several grids (odd n1 falls back to the cache-based kernel; tiles with
+    partial x/y coverage), from the default IC, 12 attempted steps vs the oracle"""
     meta, A = O.load_case("g20")
     Pm, info = O.params_from_meta(meta)
-    info = dict(info, n1=30, n2=30, n3=60)
-    sim = P.Simulation(30, 30, 60, (info["L1"], info["L2"], info["L3"]), 0, Pm, beads=O.beads(),
-                       tau=1.0, tau_min=info["tau_min"], delta=info["delta"])
+    n1, n2, n3 = dims
+    info = dict(info, n1=n1, n2=n2, n3=n3)
+    sim = P.Simulation(n1, n2, n3, (info["L1"], info["L2"], info["L3"]), 0, Pm, beads=O.beads(),
+                       tau=1.0, tau_min=info["tau_min"], delta=info["delta"], tile=FLAVOURS[flavour][0],
+                       recompute=FLAVOURS[flavour][1])
     ic = sim.interior()
     rc = sim.solve_ex(1e9, 12, 0)
     assert rc == 2
@@ -127,7 +143,7 @@ def test_matches_oracle_larger_grid():
     sim.close()
 
 
-def _loopback_run(meta, initial, nprocs, times, mode=0, gl_static=False):
+def _loopback_run(meta, initial, nprocs, times, mode=0, gl_static=False, flavour="fused32"):
     L = P.lib()
     group = C.c_void_p()
     assert L.pft_comm_init_loopback(C.byref(group), nprocs) == 0
@@ -141,7 +157,8 @@ def _loopback_run(meta, initial, nprocs, times, mode=0, gl_static=False):
             Pm, info = O.params_from_meta(meta)
             sim = P.Simulation(info["n1"], info["n2"], info["n3"], (info["L1"], info["L2"], info["L3"]), mode,
                                Pm, nprocs=nprocs, rank=r, initial=initial, tau=1.0, tau_min=info["tau_min"],
-                               delta=info["delta"], gl_static=gl_static)
+                               delta=info["delta"], gl_static=gl_static, tile=FLAVOURS[flavour][0],
+                               recompute=FLAVOURS[flavour][1])
             res = []
             for T in times:
                 rc = sim.solve(T)
@@ -166,12 +183,13 @@ def _loopback_run(meta, initial, nprocs, times, mode=0, gl_static=False):
 
 @pytest.mark.parametrize("nprocs", [2, 4])
 @pytest.mark.parametrize("gl_static", [False, True])
-def test_multislab_loopback_bitwise(nprocs, gl_static):
+@pytest.mark.parametrize("flavour", ["fused32", "tile16", "cache"])
+def test_multislab_loopback_bitwise(nprocs, gl_static, flavour):
     """Z-slab decomposition with halo exchange (boundary planes first, interior overlapped) over
     the loopback transport on one GPU: identical to the single-slab reference trajectory (F6)"""
     meta, A = O.load_case("g20")
     times = meta["traj_times"][:2]
-    out = _loopback_run(meta, A["traj_m0_ic"], nprocs, times, gl_static=gl_static)
+    out = _loopback_run(meta, A["traj_m0_ic"], nprocs, times, gl_static=gl_static, flavour=flavour)
     for i in range(len(times)):
         ref = meta["traj_m0"][i]
         for r in range(nprocs):
