@@ -33,6 +33,11 @@
 #ifndef PFT_S5_RELOAD
 #define PFT_S5_KEEP 1
 #endif
+// minimum waves per SIMD of the fused stage kernels 1-4 (stage 5 keeps ~250 VGPRs live: capped
+// at 256 so that two waves fit)
+#ifndef PFT_FUSED_WAVES
+#define PFT_FUSED_WAVES 3
+#endif
 
 static __thread char g_err[256];
 
@@ -108,6 +113,75 @@ __device__ __forceinline__ void rhs_cell(const pft_consts& c, const Col& u, cons
     double dpdt = c.h1_2 * (-(-p.xm + pc) + (-pc + p.xp)) +
                   c.h2_2 * (-(-p.ym + pc) + (-pc + p.yp)) +
                   c.h3_2 * (-(-p.zm + pc) + (-pc + p.zp));
+    if (MODE == 0 || MODE == 10) {
+      const double v1 = c.h1d2 * (-p.xm + p.xp);
+      const double v2 = c.h2d2 * (-p.ym + p.yp);
+      const double v3 = c.h3d2 * (-p.zm + p.zp);
+      const double gn = sqrt(v1 * v1 + v2 * v2 + v3 * v3) + 1E-10;
+      dpdt += c.xi2a * pc * (1.0 - pc) * (pc - 0.5) - c.bam * gn * (un - c.u_star);
+    } else {
+      dpdt += c.xi2a * pc * (1.0 - pc) * (pc - 0.5) -
+              c.sam * sshape(c, pc) * sshape(c, 1.0 - pc) * fmax(pc * (1.0 - pc), 0.0) * (un - c.u_star);
+    }
+    dpdt /= c.alpha;
+    dpdt *= wi;
+    dp = dpdt;
+    if (MODE == 0 || MODE == 1) du = (flux / rho + c.L * dpdt) / cp;
+  }
+}
+
+// The same arithmetic with face reuse: a face shared by two cells computed by one thread is
+// evaluated once.  Across the face between cells a (minus side) and b (plus side) the reference
+// computes, at a: lp * (-u_a + u_b) with lp = lambda(0.5*(p_a+p_b), 0.5*(g_a+g_b)), and at b:
+// (-lm) * (-u_a + u_b) with lm = lambda(0.5*(p_a+p_b), ...) -- the same operands in the same
+// order, so lm == lp and (-lm)*d == -(lp*d) exactly; likewise the Laplacian difference
+// (-p_a + p_b).  FaceT carries {lp*d, -p_a + p_b} from a to b.
+struct FaceT {
+  double prod, dp;
+};
+
+__device__ __forceinline__ FaceT face_of(const pft_consts& c, double pa, double ga, double ua, double pb, double gb,
+                                         double ub, bool need_flux)
+{
+  FaceT f;
+  f.dp = -pa + pb;
+  f.prod = need_flux ? lam_of(c, 0.5 * (pa + pb), 0.5 * (ga + gb)) * (-ua + ub) : 0.0;
+  return f;
+}
+
+// rhs_cell with the x-minus and z-minus faces given (fxm, fzm: the plus faces of the neighbours),
+// returning this cell's x-plus and z-plus faces
+template <int MODE>
+__device__ __forceinline__ void rhs_cell_f(const pft_consts& c, const Col& u, const Col& p, const Col& g, double un,
+                                           const FaceT& fxm, const FaceT& fzm, FaceT& fxp, FaceT& fzp, double& du,
+                                           double& dp)
+{
+  constexpr bool FLUX = MODE != 10 && MODE != 11;
+  const double pc = p.c, gc = g.c, uc = u.c;
+  const double rho = gc * c.rho_g + (1.0 - gc) * (pc * c.rho_i + (1.0 - pc) * c.rho_w);
+  const double cp = gc * c.cp_g + (1.0 - gc) * (pc * c.cp_i + (1.0 - pc) * c.cp_w);
+  const double wi = fmax(0.0, 1.0 - c.zeta * gc);
+  fxp = face_of(c, pc, gc, uc, p.xp, g.xp, u.xp, FLUX);
+  fzp = face_of(c, pc, gc, uc, p.zp, g.zp, u.zp, FLUX);
+  if (MODE == 10 || MODE == 11) du = 0.0;
+  double flux = 0.0;
+  if (FLUX) {
+    const double lym = lam_of(c, 0.5 * (p.ym + pc), 0.5 * (g.ym + gc));
+    const double lyp = lam_of(c, 0.5 * (pc + p.yp), 0.5 * (gc + g.yp));
+    flux = c.h1_2 * (-fxm.prod + fxp.prod) +
+           c.h2_2 * (-lym * (-u.ym + uc) + lyp * (-uc + u.yp)) +
+           c.h3_2 * (-fzm.prod + fzp.prod);
+  }
+  if (MODE == 2) {
+    const double ch = cosh(c.gamma * (uc - c.u_star));
+    const double dpdu = (c.mhg / (ch * ch)) * wi;
+    const double d = flux / (rho * (cp - c.L * dpdu));
+    du = d;
+    dp = dpdu * d;
+  } else {
+    double dpdt = c.h1_2 * (-fxm.dp + fxp.dp) +
+                  c.h2_2 * (-(-p.ym + pc) + (-pc + p.yp)) +
+                  c.h3_2 * (-fzm.dp + fzp.dp);
     if (MODE == 0 || MODE == 10) {
       const double v1 = c.h1d2 * (-p.xm + p.xp);
       const double v2 = c.h2d2 * (-p.ym + p.yp);
@@ -587,7 +661,7 @@ __device__ __forceinline__ void keep5(int q, const Ops& r, dbl2& x, dbl2& k1, db
 }
 
 template <int STAGE, int MODE, bool GLS, int WX>
-__global__ __launch_bounds__(PFT_BLOCK) void merson_fused(StageArgs a, pft_consts c)
+__global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu(STAGE == 5 ? 2 : PFT_FUSED_WAVES))) void merson_fused(StageArgs a, pft_consts c)
 {
   using G = TileGeo<WX>;
   __shared__ __attribute__((aligned(16))) double lds[2][3][G::LF];
@@ -619,6 +693,11 @@ __global__ __launch_bounds__(PFT_BLOCK) void merson_fused(StageArgs a, pft_const
   double m = 0.0;
   bool nf = false;
   dbl2 zm[3], zc[3], zp[3];
+  constexpr bool FLUX = MODE != 10 && MODE != 11;
+  // face reuse (rhs_cell_f) in stages 1-4; stage 5 already holds ~250 VGPRs of combine operands
+  // and the z-face carry would push it past 256 (one wave per SIMD): measured 0.58 vs 0.53 ms
+  constexpr bool FACE = STAGE != 5;
+  FaceT fz[2];                         // z-face below plane k of each cell of the pair
 #ifdef PFT_S5_KEEP
   // stage 5 keeps x, K1, K4 and the K1/K3/K4 part of the error norm of planes k and k+1
   dbl2 cx[3], ck1[3], ck4[3], cE[3], nx[3], nk1[3], nk4[3], nE[3];
@@ -647,6 +726,12 @@ __global__ __launch_bounds__(PFT_BLOCK) void merson_fused(StageArgs a, pft_const
       Ops tmp;
       load_ops<STAGE, GLS>(a, hf, (long)(kb + 1) * a.plane + hp, tmp);
       st2(&lds[0][hf][hl], stage_in<STAGE, GLS>(a, hf, tmp));
+    }
+    // the z-face below the chunk's first plane; later planes inherit it from the plane below
+    if constexpr (FACE) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        fz[s] = face_of(c, zm[1][s], zm[2][s], zm[0][s], zc[1][s], zc[2][s], zc[0][s], FLUX);
     }
     __syncthreads();
   }
@@ -677,6 +762,7 @@ __global__ __launch_bounds__(PFT_BLOCK) void merson_fused(StageArgs a, pft_const
       }
     }
     double du[2], dp[2];
+    FaceT fx;                          // the x-face between the pair's two cells
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       Col col[3];
@@ -685,21 +771,36 @@ __global__ __launch_bounds__(PFT_BLOCK) void merson_fused(StageArgs a, pft_const
         const double* L = lds[cur][q];
         const double cen = zc[q][s];
         col[q].c = cen;
-        if (s == 0) {
-          col[q].xm = i0 > 0 ? L[lo - 1] : cen;
-          col[q].xp = zc[q][1];
+        if constexpr (FACE) {
+          // every LDS address is inside the tile's halo ring: load unconditionally, select the
+          // wall mirror (equation.c:164-174) without branching
+          const double lx = s == 0 ? L[lo - 1] : L[lo + 2];
+          const double ly0 = L[lo - G::LW + s], ly1 = L[lo + G::LW + s];
+          col[q].xm = s == 0 ? (i0 > 0 ? lx : cen) : zc[q][0];
+          col[q].xp = s == 0 ? zc[q][1] : (i0 + 2 < a.n1 ? lx : cen);
+          col[q].ym = j > 0 ? ly0 : cen;
+          col[q].yp = j < a.n2 - 1 ? ly1 : cen;
         } else {
-          col[q].xm = zc[q][0];
-          col[q].xp = i0 + 2 < a.n1 ? L[lo + 2] : cen;
+          // (stage 5: the branchy form needs fewer live registers)
+          col[q].xm = s == 0 ? (i0 > 0 ? L[lo - 1] : cen) : zc[q][0];
+          col[q].xp = s == 0 ? zc[q][1] : (i0 + 2 < a.n1 ? L[lo + 2] : cen);
+          col[q].ym = j > 0 ? L[lo - G::LW + s] : cen;
+          col[q].yp = j < a.n2 - 1 ? L[lo + G::LW + s] : cen;
         }
-        col[q].ym = j > 0 ? L[lo - G::LW + s] : cen;
-        col[q].yp = j < a.n2 - 1 ? L[lo + G::LW + s] : cen;
         col[q].zm = zm[q][s];
         col[q].zp = top ? cen : zp[q][s];
       }
       if (top) col[0].zp = a.T_top;
       const double un = a.noise ? zc[0][s] + a.noise[(long)k * a.plane + po + s] : zc[0][s];
-      rhs_cell<MODE>(c, col[0], col[1], col[2], un, du[s], dp[s]);
+      if constexpr (FACE) {
+        const FaceT fxm =
+            s == 0 ? face_of(c, col[1].xm, col[2].xm, col[0].xm, col[1].c, col[2].c, col[0].c, FLUX) : fx;
+        FaceT fzp;
+        rhs_cell_f<MODE>(c, col[0], col[1], col[2], un, fxm, fz[s], fx, fzp, du[s], dp[s]);
+        fz[s] = fzp;
+      } else {
+        rhs_cell<MODE>(c, col[0], col[1], col[2], un, du[s], dp[s]);
+      }
     }
     if (more && hact) st2(&lds[cur ^ 1][hf][hl], hv);
     if (active) {
