@@ -6,9 +6,14 @@ One "step" = one attempted Merson step of RK_MPI_SA_solve (the reference's steps
 update, run by libpft's fused device path with the state resident in HBM.
 
 Workload (N = number of GPUs, one process per GPU, Z-slab decomposition, weak scaling):
-  default Params (apps/intertrack-hybrid-S-freezing/Params, calc_mode 0 GradP) at grid_nodes 400
-  -> 200 x 200 x 400 cells per GPU; with N GPUs the domain is N times taller
-  (200 x 200 x 400N cells, L3 = 0.06 N m), so every GPU holds the 400^3 slab of the 1-GPU case.
+  default Params (apps/intertrack-hybrid-S-freezing/Params, calc_mode 0 GradP).  "G^3" means
+  grid_nodes G, i.e. (G/2) x (G/2) x G cells of the fixed 0.03 x 0.03 x 0.06 m domain.
+  N = 1: 400^3 = 200 x 200 x 400 = 16 M cells.
+  --shape cube (default): G = 400 N^(1/3) rounded to a multiple of 4, so N = 8 is exactly the
+      "800^3 grid, 8-way Z-slab split" configuration (400 x 400 x 800, 100 planes per GPU) and
+      every GPU holds ~16 M cells (N = 2: 504^3, N = 4: 636^3).
+  --shape tall: the 400^3 slab stacked N times (200 x 200 x 400N, L3 = 0.06 N m): per-GPU work
+      identical to N = 1, only the halo exchange is added.
   Initial state: the default Params initial condition (u = 293.15 K, ice cap, glass walls and
   200 glass beads) built by libpft's host model code; t = 0, h = tau = 1 s.
 
@@ -50,7 +55,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--grid-nodes", type=int, default=400, help="grid_nodes of the per-GPU slab")
+    ap.add_argument("--grid-nodes", type=int, default=400, help="grid_nodes G of the 1-GPU case")
+    ap.add_argument("--shape", choices=("cube", "tall"), default="cube",
+                    help="N>1 weak-scaling family (module docstring)")
+    ap.add_argument("--literal-cube", action="store_true",
+                    help="L1 = L2 = L3 = 0.06 m: G x G x G cells (SURVEY 8(d) secondary number)")
     ap.add_argument("--mode", type=int, default=0, help="calc_mode (0 GradP, 1 SigmaP1-P, 2 Temp)")
     ap.add_argument("--gl-static", action="store_true", help="exploit dgl == 0 (bit-identical)")
     ap.add_argument("--kz", type=int, default=0, help="planes per workgroup z-march (default 8)")
@@ -58,7 +67,8 @@ def parse():
     ap.add_argument("--no-recompute", action="store_true",
                     help="materialise the reference's aux arrays between stages (72 vs 54 doubles/cell-step)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
-    ap.add_argument("--cpu-steps", type=int, default=3, help="attempted steps of the CPU sample")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="CPU sample: attempted steps (in batches of 2) until this much time has passed")
     ap.add_argument("--no-timing", action="store_true", help="no HIP-event stage timing")
     ap.add_argument("--probe", type=int, default=0,
                     help="after the run, launch the 8-B/lane copy probe this many times "
@@ -106,10 +116,7 @@ def main():
         L.pft_hip_device_sync()
 
     # ---- workload -------------------------------------------------------------------------
-    base = PR.default_params(grid_nodes=a.grid_nodes, calc_mode=a.mode)
-    n1, n2, n3_slab = base["n1"], base["n2"], base["n3"]
-    total_n3 = n3_slab * world
-    Ls = (base["L1"], base["L2"], base["L3"] * world)
+    gn, base, (n1, n2, total_n3), Ls = workload(a.grid_nodes, world, a.shape, a.literal_cube, a.mode)
     prm = P.params_array(base)
     beads = np.load(os.path.join(REPO, "tests", "golden", "beads.npy"))
     t0 = time.time()
@@ -160,13 +167,13 @@ def main():
         if os.path.exists(pmc):
             try:
                 ps = json.load(open(pmc))
-                key = f"stage{dom}_gl{int(a.gl_static)}_g{a.grid_nodes}_m{a.mode}"
+                key = f"stage{dom}_gl{int(a.gl_static)}_g{gn}_n{world}_m{a.mode}"
                 traffic = ps.get(key, {}).get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                "kernel": f"merson_stage<{dom},{a.mode},{'true' if a.gl_static else 'false'}>",
+                "kernel": kernel_name(dom, a, rc_path, n1),
                 "algorithmic_bytes_per_launch": byts,
                 "avg_launch_ms": round(ms, 4),
                 "stages_ms": {str(s): round(per[s][0], 4) for s in per},
@@ -188,8 +195,11 @@ def main():
         "dtype": "f64",
         "data": "synthetic: default Params initial condition (u=293.15 K, ice cap, glass walls, "
                 "200 glass beads from the reference's data file), t=0, h=tau=1",
-        "config": {"workload": f"{a.grid_nodes}^3 default Params per GPU: {n1}x{n2}x{n3_slab} cells/GPU, "
-                               f"global {n1}x{n2}x{total_n3} (Z-slab weak scaling)",
+        "config": {"workload": (f"{gn}^3 default Params" if a.shape == "cube" or world == 1 else
+                                f"{a.grid_nodes}^3 slab x {world} (tall)") +
+                               f": {n1}x{n2}x{total_n3} cells, Z-slab split {world}-way "
+                               f"({n1}x{n2}x{sim.grid.n3} on rank {rank})",
+                   "grid_nodes": gn, "shape": a.shape, "literal_cube": a.literal_cube,
                    "calc_mode": a.mode, "cells": cells_total, "parallelism": f"zslab{world}",
                    "gl_static": a.gl_static, "kz": a.kz or 8, "tile": a.tile, "recompute": not a.no_recompute,
                    "accepted_steps_total": int(sim.system.steps), "t_end": sim.t},
@@ -228,6 +238,28 @@ def main():
         dist.destroy_process_group()
 
 
+def workload(grid_nodes, world, shape="cube", literal_cube=False, mode=0):
+    """(G, Params dict, (n1, n2, total_n3), (L1, L2, L3)) of the N = world benchmark case"""
+    Lc = (PR.float_val("0.06"),) * 3 if literal_cube else None
+    if shape == "cube" and world > 1:
+        gn = int(round(grid_nodes * world ** (1.0 / 3.0) / 4.0)) * 4
+        base = PR.default_params(grid_nodes=gn, calc_mode=mode, L=Lc)
+        return gn, base, (base["n1"], base["n2"], base["n3"]), (base["L1"], base["L2"], base["L3"])
+    base = PR.default_params(grid_nodes=grid_nodes, calc_mode=mode, L=Lc)
+    return (grid_nodes, base, (base["n1"], base["n2"], base["n3"] * world),
+            (base["L1"], base["L2"], base["L3"] * world))
+
+
+def kernel_name(stage, a, rc_path, n1):
+    """the stage kernel libpft launches for these options (pft_kernels.hip launch_stage)"""
+    gls = "true" if a.gl_static else "false"
+    if a.tile == 0 or n1 % 2:
+        return f"merson_stage<{stage}, {a.mode}, {gls}>"
+    if rc_path:
+        return f"merson_fused<{stage}, {a.mode}, {gls}, {a.tile}>"
+    return f"merson_tile<{stage}, {a.mode}, {gls}, {a.tile}>"
+
+
 def cpu_baseline(sim, base, a):
     """Time the CPU restatement of the reference (oracle/pft_oracle.c: plain C, OpenMP over
     z-planes, the reference's arithmetic) on the same 400^3 state for a few attempted steps."""
@@ -246,16 +278,24 @@ def cpu_baseline(sim, base, a):
     xp = O.pad(og, x0)
     t, h = C.c_double(sim.t), C.c_double(sim.h)
     s, stt = C.c_long(0), C.c_long(0)
-    t0 = time.perf_counter()
-    O.lib().pft_or_solve(C.byref(og), O.ptr(prm), a.mode, base["final_time"], C.byref(t), C.byref(h),
-                         base["tau_min"], base["delta"], 0, O.ptr(xp), C.byref(s), C.byref(stt),
-                         a.cpu_steps, O.EXCHANGE_FN(), O.ALLREDUCE_FN(), None)
-    el = time.perf_counter() - t0
+
+    def run(nsteps):
+        # the cap counts this call's attempted steps; (t, h) carry the trajectory on
+        t0 = time.perf_counter()
+        O.lib().pft_or_solve(C.byref(og), O.ptr(prm), a.mode, base["final_time"], C.byref(t), C.byref(h),
+                             base["tau_min"], base["delta"], 0, O.ptr(xp), C.byref(s), C.byref(stt),
+                             nsteps, O.EXCHANGE_FN(), O.ALLREDUCE_FN(), None)
+        return time.perf_counter() - t0
+
+    probe = run(1)                                   # sizes the sample (not counted)
+    n = max(2, int(a.cpu_seconds / probe))
+    stt.value = 0
+    el = run(n)
     cores = int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count() or 1)))
     cells = g.n1 * g.n2 * g.total_n3
     return {"value": round(cells * stt.value / el / 1e6, 3), "unit": "Mcells·steps/s", "cores": cores,
             "kind": "port",
-            "sample": f"{stt.value} attempted steps of the same {g.n1}x{g.n2}x{g.total_n3} state, "
+            "sample": f"{stt.value} attempted steps of the same {g.n1}x{g.n2}x{g.total_n3} state (after 1 untimed), "
                       f"oracle/pft_oracle.c (gcc -O2, OpenMP {cores} threads), {el:.1f} s"}
 
 

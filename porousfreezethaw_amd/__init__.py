@@ -79,7 +79,7 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"libpft.so is not built ({LIB_PATH}); run __graft_entry__.build()")
-        L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        L = C.CDLL(LIB_PATH)   # RTLD_LOCAL: its ROCm 7.2 runtime must not interpose on torch's
         dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int)
         L.RK_MPI_SA_init.argtypes = [C.c_int, C.c_int, C.c_int]
         L.RK_MPI_SA_check_mem.argtypes = [C.POINTER(RK_MEM_DIST)]

@@ -1,0 +1,32 @@
+#!/bin/bash
+# One GPU-box session producing the round's evidence (TAG=r01 by default):
+#   1. pytest -m gpu, smoke()
+#   2. rocprofv3 --kernel-trace --stats of a short bench run, then FETCH_SIZE and WRITE_SIZE in
+#      separate --pmc passes (never combined with other tracing) -> profiles/pmc_summary.json
+#   3. the default bench line (reads profiles/pmc_summary.json for roofline.traffic), then the
+#      secondary numbers of SURVEY 8(d): calc_mode 1 and 2, gl_static, the literal 400^3 cube
+# Every GPU step runs under its own time limit; a crash/fault/timeout ends the script.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+TAG=${TAG:-r01}
+O=gpurun_out/ev
+mkdir -p $O/prof
+fatal() { local rc=$1; echo "[$2] exit $rc" | tee -a $O/status.log
+  if [ "$rc" -ge 124 ] || [ "$rc" -eq 134 ] || [ "$rc" -eq 139 ]; then echo "fatal in $2, stopping"; exit "$rc"; fi; }
+if [ -z "$SKIP_TESTS" ]; then
+  timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $O/pytest_gpu.log 2>&1; fatal $? pytest
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1; fatal $? smoke
+fi
+ARGS="--steps 20 --warmup 3 --no-cpu --probe 3"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof/trace -o run --output-format csv -- python3 bench.py $ARGS > $O/prof/trace_bench.json 2> $O/prof/trace.err; fatal $? trace
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $O/prof/fetch -o run --output-format csv -- python3 bench.py $ARGS > $O/prof/fetch_bench.json 2> $O/prof/fetch.err; fatal $? fetch
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $O/prof/write -o run --output-format csv -- python3 bench.py $ARGS > $O/prof/write_bench.json 2> $O/prof/write.err; fatal $? write
+PB=$(python3 -c "import json;print(json.load(open('$O/prof/trace_bench.json'))['probe_bytes_each_way'])")
+python3 scripts/pmc_summary.py $O/prof/trace $O/prof/fetch $O/prof/write 400 $PB $O/pmc_summary.json > $O/pmc_summary.txt 2>&1; fatal $? pmc_summary
+cp $O/pmc_summary.json profiles/pmc_summary.json
+timeout -k 10 900 python bench.py > $O/bench_default.json 2> $O/bench_default.err; fatal $? bench_default
+timeout -k 10 300 python bench.py --steps 100 --no-cpu --mode 1 > $O/bench_mode1.json 2>> $O/bench_var.err; fatal $? bench_mode1
+timeout -k 10 300 python bench.py --steps 100 --no-cpu --mode 2 > $O/bench_mode2.json 2>> $O/bench_var.err; fatal $? bench_mode2
+timeout -k 10 300 python bench.py --steps 100 --no-cpu --gl-static > $O/bench_gls.json 2>> $O/bench_var.err; fatal $? bench_gls
+timeout -k 10 600 python bench.py --steps 50 --no-cpu --literal-cube > $O/bench_cube64M.json 2>> $O/bench_var.err; fatal $? bench_cube
+echo done >> $O/status.log

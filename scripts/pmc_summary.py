@@ -6,7 +6,7 @@ runs (FETCH_SIZE, WRITE_SIZE -- separate passes, MI355X_MICROARCH.md "rocprofv3 
 Corrections (MI355X_MICROARCH.md "HBM"): FETCH_SIZE/WRITE_SIZE are in KiB; gfx950's FETCH_SIZE
 is only exact for calibrated access widths, so the ratio known/measured of the probe_copy_kernel
 (8-byte loads and stores per lane, exactly the stage kernels' width, known byte count) calibrates
-both counters.  Output keys: stage<k>_gl<0|1>_g<grid>_m<mode> -> HBM bytes per launch.
+both counters.  Output keys: stage<k>_gl<0|1>_g<grid>_n1_m<mode> -> HBM bytes per launch.
 """
 import csv
 import glob
@@ -35,7 +35,7 @@ def counters(d, name):
 
 
 def kname(k):
-    m = re.search(r"merson_stage<(\d+),\s*(\d+),\s*(true|false)>", k)
+    m = re.search(r"merson_(?:stage|tile|fused)<(\d+),\s*(\d+),\s*(true|false)", k)
     if m:
         return f"stage{m.group(1)}", m.group(2), m.group(3) == "true"
     if "probe_copy" in k:
@@ -62,7 +62,7 @@ def main(trace_dir, fetch_dir, write_dir, grid, probe_bytes, out_path):
             continue
         fb = fetch.get(k, 0.0) * 1024 * cal_f
         wb = write.get(k, 0.0) * 1024 * cal_w
-        key = f"{st}_gl{int(gls)}_g{grid}_m{mode}"
+        key = f"{st}_gl{int(gls)}_g{grid}_n1_m{mode}"
         res[key] = {"kernel": k, "fetch_bytes": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
                     "raw_FETCH_SIZE_KiB": fetch.get(k), "raw_WRITE_SIZE_KiB": write.get(k)}
     res["kernel_stats"] = stats
