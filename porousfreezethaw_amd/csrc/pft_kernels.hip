@@ -1047,25 +1047,20 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
   s->n1_tiled_ok = 1;
   s->recompute = 1;
   const size_t bytes = sizeof(double) * 3 * (size_t)s->fs;
-  for (int b = 0; b < PFT_BUF_COUNT; ++b) {
-    hipError_t e = hipMalloc((void**)&s->buf[b], bytes);
-    if (e != hipSuccess) {
-      pft_slab_destroy(s);
-      return fail(e, "hipMalloc(state)");
-    }
-    e = hipMemset(s->buf[b], 0, bytes);
-    if (e != hipSuccess) {
-      pft_slab_destroy(s);
-      return fail(e, "hipMemset(state)");
-    }
-  }
-  hipError_t e = hipMalloc((void**)&s->scratch, 64);
-  if (e == hipSuccess) e = hipHostMalloc((void**)&s->host_scratch, 64, hipHostMallocDefault);
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+  hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->comm, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc((void**)&s->scratch, 64);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&s->host_scratch, 64, hipHostMallocDefault);
+  for (int b = 0; b < PFT_BUF_COUNT && e == hipSuccess; ++b) {
+    e = hipMalloc((void**)&s->buf[b], bytes);
+    // zero-fill on the slab's own stream: the compute stream is non-blocking, so a fill on the
+    // null stream would not be ordered before the first upload/kernel (it raced with them)
+    if (e == hipSuccess) e = hipMemsetAsync(s->buf[b], 0, bytes, s->stream);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
   if (e != hipSuccess) {
     pft_slab_destroy(s);
-    return fail(e, "slab scratch/streams");
+    return fail(e, "slab buffers/streams");
   }
   *out = s;
   return 0;
