@@ -263,3 +263,61 @@ def test_nan_handling_gives_up():
     finally:
         P.lib().RK_MPI_SA_handle_NAN(0)
         sim.close()
+
+
+def _full_size_case():
+    from porousfreezethaw_amd import params as PR
+    base = PR.default_params(grid_nodes=400, calc_mode=0)
+    info = {k: base[k] for k in ("n1", "n2", "n3", "L1", "L2", "L3", "tau_min", "delta")}
+    return base, P.params_array(base), info
+
+
+def test_full_size_400_bitwise_and_rank_invariant():
+    """BASELINE's 400^3 (200x200x400, default Params, beads) at full size: 3 attempted steps of the
+    device path equal the oracle bit for bit, and a 2-slab loopback run (halo exchange, boundary
+    planes first) equals the single-slab one (rank-count invariance)"""
+    base, Pm, info = _full_size_case()
+    L3s = (info["L1"], info["L2"], info["L3"])
+    sim = P.Simulation(info["n1"], info["n2"], info["n3"], L3s, 0, Pm, beads=O.beads(), tau=1.0,
+                       tau_min=info["tau_min"], delta=info["delta"])
+    ic = sim.interior()
+    assert sim.solve_ex(1e9, 3, 0) == 2
+    got = (sim.t, sim.h, sim.system.steps, sim.system.steps_total)
+    x1 = sim.interior()
+    sim.close()
+    res = O.solve(info, Pm, 0, ic, 0.0, 1.0, [1e9], max_steps_total=3)[0]
+    assert got == tuple(res[:4])
+    assert np.array_equal(x1, res[5])
+    del res
+
+    L = P.lib()
+    group = C.c_void_p()
+    assert L.pft_comm_init_loopback(C.byref(group), 2) == 0
+    out, errs = [None, None], []
+
+    def worker(r):
+        try:
+            mine = C.c_void_p()
+            assert L.pft_comm_loopback_rank(group, r, C.byref(mine)) == 0
+            L.pft_comm_set_current(mine)
+            s = P.Simulation(info["n1"], info["n2"], info["n3"], L3s, 0, Pm, nprocs=2, rank=r, initial=ic,
+                             tau=1.0, tau_min=info["tau_min"], delta=info["delta"])
+            assert s.solve_ex(1e9, 3, 0) == 2
+            out[r] = ((s.t, s.h, s.system.steps, s.system.steps_total), s.interior())
+            s.close()
+            L.pft_comm_set_current(None)
+            L.pft_comm_destroy(mine)
+        except BaseException as e:  # noqa: BLE001 -- surfaced below
+            errs.append(e)
+
+    ths = [threading.Thread(target=worker, args=(r,)) for r in range(2)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=600)
+    L.pft_comm_destroy(group)
+    if errs:
+        raise errs[0]
+    for r in range(2):
+        assert out[r][0] == got
+    assert np.array_equal(np.concatenate([out[0][1], out[1][1]], axis=1), x1)
