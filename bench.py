@@ -63,8 +63,9 @@ def parse():
                     help="L1 = L2 = L3 = 0.06 m: G x G x G cells (SURVEY 8(d) secondary number)")
     ap.add_argument("--mode", type=int, default=0, help="calc_mode (0 GradP, 1 SigmaP1-P, 2 Temp)")
     ap.add_argument("--gl-static", action="store_true", help="exploit dgl == 0 (bit-identical)")
-    ap.add_argument("--kz", type=int, default=0, help="planes per workgroup z-march (default 8)")
-    ap.add_argument("--tile", type=int, default=32, help="32 / 16: LDS-tiled kernel, 0: cache-based")
+    ap.add_argument("--kz", type=int, default=0, help="planes per workgroup z-march (default 0 = automatic)")
+    ap.add_argument("--tile", type=int, default=1,
+                    help="1: per stage (default), 32 / 16: LDS-tiled kernel, 0: cache-based")
     ap.add_argument("--no-recompute", action="store_true",
                     help="materialise the reference's aux arrays between stages (72 vs 54 doubles/cell-step)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
@@ -92,6 +93,10 @@ def main():
             sys.exit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
         a.gpus = world
     L = P.lib()
+    ndev = P.device_count()
+    if ndev < 1:
+        sys.exit("no HIP device visible (the benchmark has no CPU fallback)")
+    dev = local % ndev           # one process per GPU; more ranks than GPUs share round-robin
     dist = None
     comm = None
     if world > 1:
@@ -106,13 +111,13 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         uid = (C.c_char * 128).from_buffer_copy(obj[0])
         comm = C.c_void_p()
-        rc = L.pft_comm_init_rccl(C.byref(comm), world, rank, uid, local)
+        rc = L.pft_comm_init_rccl(C.byref(comm), world, rank, uid, dev)
         if rc:
             sys.exit(f"rank {rank}: pft_comm_init_rccl failed ({rc})")
         L.pft_comm_set_current(comm)
     else:
-        L.pft_hip_set_device(local)
-    L.pft_solver_set_option(P.PFT_OPT_DEVICE, local)
+        L.pft_hip_set_device(dev)
+    L.pft_solver_set_option(P.PFT_OPT_DEVICE, dev)
 
     def barrier():
         if dist is not None:
@@ -210,7 +215,7 @@ def main():
                                f"({n1}x{n2}x{sim.grid.n3} on rank {rank})",
                    "grid_nodes": gn, "shape": a.shape, "literal_cube": a.literal_cube,
                    "calc_mode": a.mode, "cells": cells_total, "parallelism": f"zslab{world}",
-                   "gl_static": a.gl_static, "kz": a.kz or 8, "tile": a.tile, "recompute": not a.no_recompute,
+                   "gl_static": a.gl_static, "kz": a.kz or "auto", "tile": a.tile, "recompute": not a.no_recompute,
                    "accepted_steps_total": int(sim.system.steps), "t_end": sim.t,
                    "host_boundary": a.host_boundary},
         "roofline": roof,
@@ -265,9 +270,10 @@ def kernel_name(stage, a, rc_path, n1):
     gls = "true" if a.gl_static else "false"
     if a.tile == 0 or n1 % 2:
         return f"merson_stage<{stage}, {a.mode}, {gls}>"
+    wx = (16 if stage <= 2 else 32) if a.tile == 1 else a.tile
     if rc_path:
-        return f"merson_fused<{stage}, {a.mode}, {gls}, {a.tile}>"
-    return f"merson_tile<{stage}, {a.mode}, {gls}, {a.tile}>"
+        return f"merson_fused<{stage}, {a.mode}, {gls}, {wx}>"
+    return f"merson_tile<{stage}, {a.mode}, {gls}, {wx}>"
 
 
 def cpu_baseline(sim, base, a):

@@ -73,10 +73,12 @@ size_t pft_slab_plane(const pft_slab * s);            /* n1*n2 */
 int pft_slab_nz(const pft_slab * s);                  /* n3 (interior planes) */
 void * pft_slab_scratch(pft_slab * s);                /* device: u64 eps bits, u64 non-finite flag */
 const pft_slab_desc * pft_slab_get_desc(const pft_slab * s);
-/* planes per workgroup z-march (tuning knob, default 16) */
+/* planes per workgroup z-march (tuning knob); 0 (default) = automatic: the fewest planes per
+   workgroup that keep the whole launch resident in one round (occupancy x CUs / tiles chunks) */
 int pft_slab_set_kz(pft_slab * s, int kz);
-/* stage kernel flavour: 32 (default) or 16 = LDS-tiled kernel with 64x8 / 32x16 cell tiles
-   (n1 even); 0 = cache-based kernel (any n1; also used automatically for odd n1) */
+/* stage kernel flavour: 32 or 16 = LDS-tiled kernel with 64x8 / 32x16 cell tiles (n1 even);
+   1 (default) = per stage (32x16 for the VALU-bound stages 1-2, 64x8 for 3-5); 0 = cache-based
+   kernel (any n1; also used automatically for odd n1) */
 int pft_slab_set_tile(pft_slab * s, int wx);
 /* 1 (default): the tiled kernels rebuild every stage input from x and the K's inside the
    stencil (no aux arrays: 54 instead of 72 doubles of traffic per cell-step, bit-identical);

@@ -30,11 +30,12 @@ int pft_solver_download(RK_MPI_S_SOLUTION * system);
 enum {
 	PFT_OPT_GL_STATIC = 1,  /* 1: exploit dgl == 0 (equation.c:731,874): gl neither stored in K
 	                           nor combined -- bit-identical results, less traffic. Default 0. */
-	PFT_OPT_KZ = 2,         /* planes per workgroup z-march (default 8) */
+	PFT_OPT_KZ = 2,         /* planes per workgroup z-march; 0 (default) = automatic: one full
+	                           round of resident workgroups (pft_slab_set_kz) */
 	PFT_OPT_DEVICE = 3,     /* HIP device of this thread's slab (default: current device) */
 	PFT_OPT_TIMING = 4,     /* 1: time every stage with HIP events (stats.stage_ms) */
-	PFT_OPT_TILE = 5,       /* stage kernel: 32 (default) / 16 = LDS-tiled 64x8 / 32x16 tiles,
-	                           0 = cache-based kernel (pft_slab_set_tile) */
+	PFT_OPT_TILE = 5,       /* stage kernel: 1 (default) = per stage, 32 / 16 = LDS-tiled 64x8 /
+	                           32x16 tiles, 0 = cache-based kernel (pft_slab_set_tile) */
 	PFT_OPT_RECOMPUTE = 6   /* 1 (default): rebuild stage inputs from x and the K's inside the
 	                           stencil, 0: materialise the aux arrays (pft_slab_set_recompute) */
 };

@@ -201,8 +201,8 @@ class Simulation:
         self.system = RK_MPI_S_SOLUTION(C.pointer(self.mem), t0, _dp(self.x), self.meta_addr, tau,
                                         tau_min, delta, DELTA_GLOBAL, None, None, 0, 0)
         L_.pft_solver_set_option(PFT_OPT_GL_STATIC, 1 if gl_static else 0)
-        L_.pft_solver_set_option(PFT_OPT_KZ, kz or 8)
-        L_.pft_solver_set_option(PFT_OPT_TILE, 32 if tile is None else tile)
+        L_.pft_solver_set_option(PFT_OPT_KZ, kz or 0)   # 0: automatic
+        L_.pft_solver_set_option(PFT_OPT_TILE, 1 if tile is None else tile)   # 1: per stage
         L_.pft_solver_set_option(PFT_OPT_RECOMPUTE, 1 if recompute else 0)
         self.initialised = False
         if L_.AllocPrecalcData():

@@ -18,6 +18,8 @@
 // workgroup id is remapped so that the 8 XCDs each take a contiguous run of tiles (their y
 // neighbours then share the XCD's L2, cdna_hip_programming.md T1).
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -996,9 +998,10 @@ struct pft_slab {
   unsigned long long* scratch;  // [0] eps bits, [1] nonfinite flag
   unsigned long long* host_scratch;  // pinned
   hipStream_t stream, comm;
-  int kz;
+  int kz;                // planes per workgroup z-march; 0 = automatic (one full round, see auto_kz)
+  int n_cu;               // compute units of the slab's device
   double* noise;         // device u_noise (n3*plane) or null
-  int tile_wx;           // 32 / 16: LDS-tiled kernels with that many threads per row; 0: cache-based
+  int tile_wx;           // 32 / 16: LDS-tiled kernels with that many threads per row; 1: per stage; 0: cache-based
   int n1_tiled_ok;
   int recompute;         // 1: stage inputs rebuilt from x and the K's (no aux arrays)
   hipEvent_t tev[6][2];  // per-stage timing events
@@ -1042,8 +1045,8 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
   const long raw = (long)(d->n3 + 2) * s->plane;
   s->fs = (raw + 63) & ~63L;  // 512-byte aligned field starts
   s->S = (long)(d->n1 + 4) * (d->n2 + 4) * (d->n3 + 4);
-  s->kz = 8;
-  s->tile_wx = 32;
+  s->kz = 0;
+  s->tile_wx = 1;
   s->n1_tiled_ok = 1;
   s->recompute = 1;
   const size_t bytes = sizeof(double) * 3 * (size_t)s->fs;
@@ -1058,6 +1061,9 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
     if (e == hipSuccess) e = hipMemsetAsync(s->buf[b], 0, bytes, s->stream);
   }
   if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+  int dev = 0;
+  if (e == hipSuccess) e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&s->n_cu, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) {
     pft_slab_destroy(s);
     return fail(e, "slab buffers/streams");
@@ -1095,14 +1101,14 @@ void* pft_slab_scratch(pft_slab* s) { return (void*)s->scratch; }
 const pft_slab_desc* pft_slab_get_desc(const pft_slab* s) { return &s->d; }
 int pft_slab_set_tile(pft_slab* s, int wx)
 {
-  if (wx != 0 && wx != 16 && wx != 32) return -2;
+  if (wx != 0 && wx != 1 && wx != 16 && wx != 32) return -2;
   s->tile_wx = wx;
   return 0;
 }
 
 int pft_slab_set_kz(pft_slab* s, int kz)
 {
-  if (kz < 1) return -2;
+  if (kz < 0) return -2;
   s->kz = kz;
   return 0;
 }
@@ -1146,6 +1152,48 @@ int pft_slab_download_host(pft_slab* s, int which, double* host_padded)
 // kernel flavours: KCACHE (any n1, aux arrays), KTILE (LDS tile, aux arrays), KFUSED (LDS tile,
 // stage inputs recomputed from x and the K's -- the default for even n1)
 enum { KCACHE = 0, KTILE = 1, KFUSED = 2 };
+
+// resident workgroups per CU of the kernel launch_kernel would run (hipOccupancy..., cached)
+template <int STAGE, int MODE, bool GLS>
+static int kernel_occupancy(int kind, int wx)
+{
+  static int cache[3][2] = {{0, 0}, {0, 0}, {0, 0}};
+  int& n = cache[kind][wx == 16 ? 1 : 0];
+  if (n) return n;
+  const void* f = kind == KFUSED ? (wx == 16 ? (const void*)merson_fused<STAGE, MODE, GLS, 16>
+                                             : (const void*)merson_fused<STAGE, MODE, GLS, 32>)
+                : kind == KTILE ? (wx == 16 ? (const void*)merson_tile<STAGE, MODE, GLS, 16>
+                                            : (const void*)merson_tile<STAGE, MODE, GLS, 32>)
+                                : (const void*)merson_stage<STAGE, MODE, GLS>;
+  int b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, PFT_BLOCK, 0) != hipSuccess || b < 1) b = 1;
+  n = b;
+  return n;
+}
+
+template <int STAGE, bool GLS>
+static int occupancy_mode(int mode, int kind, int wx)
+{
+  switch (mode) {
+    case 0: return kernel_occupancy<STAGE, 0, GLS>(kind, wx);
+    case 1: return kernel_occupancy<STAGE, 1, GLS>(kind, wx);
+    case 2: return kernel_occupancy<STAGE, 2, GLS>(kind, wx);
+    case 10: return kernel_occupancy<STAGE, 10, GLS>(kind, wx);
+    default: return kernel_occupancy<STAGE, 11, GLS>(kind, wx);
+  }
+}
+
+static int stage_occupancy(int stage, int mode, int gls, int kind, int wx)
+{
+  switch (stage) {
+    case 0: return gls ? occupancy_mode<0, true>(mode, kind, wx) : occupancy_mode<0, false>(mode, kind, wx);
+    case 1: return gls ? occupancy_mode<1, true>(mode, kind, wx) : occupancy_mode<1, false>(mode, kind, wx);
+    case 2: return gls ? occupancy_mode<2, true>(mode, kind, wx) : occupancy_mode<2, false>(mode, kind, wx);
+    case 3: return gls ? occupancy_mode<3, true>(mode, kind, wx) : occupancy_mode<3, false>(mode, kind, wx);
+    case 4: return gls ? occupancy_mode<4, true>(mode, kind, wx) : occupancy_mode<4, false>(mode, kind, wx);
+    default: return gls ? occupancy_mode<5, true>(mode, kind, wx) : occupancy_mode<5, false>(mode, kind, wx);
+  }
+}
 
 template <int STAGE, int MODE, bool GLS>
 static void launch_kernel(int kind, int wx, dim3 g, hipStream_t st, const StageArgs& a, const pft_consts& c)
@@ -1239,15 +1287,39 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   a.has_above = s->d.has_above;
   a.k_begin = k_begin;
   a.k_end = k_end;
-  a.kz = s->kz;
-  const int wx = kind == KCACHE ? 0 : s->tile_wx;
+  // tile width: 1 = per stage (measured at 400^3: the VALU-bound stages 0-2 run faster on 32x16
+  // tiles -- fewer idle lanes at the x edge, 200 = 6.25 x 32 -- the HBM-bound stages 3-5 on 64x8)
+  const int wx = kind == KCACHE ? 0 : s->tile_wx == 1 ? (stage <= 2 ? 16 : 32) : s->tile_wx;
   if (wx) {
     const int TX = 2 * wx, TY = PFT_BLOCK / wx;
     a.ntile = ((s->d.n1 + TX - 1) / TX) * ((s->d.n2 + TY - 1) / TY);
   } else {
     a.ntile = (s->plane + PFT_BLOCK - 1) / PFT_BLOCK;
   }
-  a.nchunk = (k_end - k_begin + a.kz - 1) / a.kz;
+  const int nplanes = k_end - k_begin;
+  if (s->kz > 0) {
+    a.kz = s->kz;
+  } else {
+    // automatic: the whole launch resident in one round (a second, partial round of workgroups
+    // costs more than a longer z-march, and every chunk boundary re-reads two planes of all
+    // operands).  VALU-bound stages 1-2 take the most chunks that fit (every resident wave
+    // helps); HBM-bound stages 3-5 take the chunk count that spreads the workgroups most evenly
+    // over the CUs (measured at 400^3, 100 tiles: 500 workgroups = 2 per CU beat 700 = 2-3 per CU).
+    const int occ = stage_occupancy(stage, mode, gls, kind, wx);
+    const int max_nch = std::max(1, std::min(nplanes, s->n_cu * occ / a.ntile));
+    int best_nch = max_nch;
+    if (stage >= 3) {
+      double best_even = -1.0;
+      for (int nch = 1; nch <= max_nch; ++nch) {
+        const long nb = (long)a.ntile * nch;
+        const long m = (nb + s->n_cu - 1) / s->n_cu;            // workgroups on the busiest CU
+        const double even = (double)nb / (double)(m * s->n_cu);
+        if (even >= best_even) { best_even = even; best_nch = nch; }
+      }
+    }
+    a.kz = (nplanes + best_nch - 1) / best_nch;
+  }
+  a.nchunk = (nplanes + a.kz - 1) / a.kz;
   a.T_top = t_stage < s->c.phase_switch_time ? s->c.top_temp1 : s->c.top_temp2;
   a.coef = coef;
   a.h = h;

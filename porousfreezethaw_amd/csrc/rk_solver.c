@@ -44,7 +44,7 @@ typedef struct {
 	pft_solver_stats stats;
 } solver_state;
 
-static __thread solver_state R = { .slab_dev = -1, .opt_kz = 8, .opt_dev = -1, .opt_tile = 32 };
+static __thread solver_state R = { .slab_dev = -1, .opt_kz = 0, .opt_dev = -1, .opt_tile = 1 };
 
 static pft_comm * comm(void)
 {
@@ -117,7 +117,7 @@ int pft_solver_set_option(int opt, long value)
 {
 	switch(opt) {
 		case PFT_OPT_GL_STATIC: R.opt_gls = value ? 1 : 0; return 0;
-		case PFT_OPT_KZ: if(value < 1) return -2; R.opt_kz = (int)value; if(R.slab) pft_slab_set_kz(R.slab, R.opt_kz); return 0;
+		case PFT_OPT_KZ: if(value < 0) return -2; R.opt_kz = (int)value; if(R.slab) pft_slab_set_kz(R.slab, R.opt_kz); return 0;
 		case PFT_OPT_DEVICE: R.opt_dev = (int)value; return 0;
 		case PFT_OPT_TIMING: R.opt_timing = value ? 1 : 0; return 0;
 		case PFT_OPT_RECOMPUTE:

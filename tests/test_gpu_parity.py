@@ -24,7 +24,7 @@ def need_gpu():
 
 # kernel flavours: (tile width, recompute stage inputs)
 FLAVOURS = {"cache": (0, False), "tile32": (32, False), "tile16": (16, False),
-            "fused32": (32, True), "fused16": (16, True)}
+            "fused32": (32, True), "fused16": (16, True), "default": (1, True)}
 
 
 def make_sim(meta, initial, mode=None, flavour=None, **kw):
@@ -183,7 +183,7 @@ def _loopback_run(meta, initial, nprocs, times, mode=0, gl_static=False, flavour
 
 @pytest.mark.parametrize("nprocs", [2, 4])
 @pytest.mark.parametrize("gl_static", [False, True])
-@pytest.mark.parametrize("flavour", ["fused32", "tile16", "cache"])
+@pytest.mark.parametrize("flavour", ["default", "fused32", "tile16", "cache"])
 def test_multislab_loopback_bitwise(nprocs, gl_static, flavour):
     """Z-slab decomposition with halo exchange (boundary planes first, interior overlapped) over
     the loopback transport on one GPU: identical to the single-slab reference trajectory (F6)"""
