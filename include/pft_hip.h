@@ -118,10 +118,21 @@ int pft_slab_eps_fetch(pft_slab * s, double * eps, int * nonfinite);
    mark(stage, 0|1) records the begin/end event of one stage's launches; collect() adds the
    elapsed milliseconds of every completed begin/end pair to ms[1..5] and counts to n[1..5] */
 int pft_slab_timing_mark(pft_slab * s, int stage, int end);
-int pft_slab_timing_collect(pft_slab * s, double * ms, long * n);
+int pft_slab_timing_collect(pft_slab * s, double * ms, long * n);   /* completed pairs only */
+int pft_slab_timing_flush(pft_slab * s, double * ms, long * n);     /* waits for all pairs */
 
 /* buffer swap X <-> XN after an accepted step */
 int pft_slab_accept(pft_slab * s);
+int pft_slab_swap_buffers(pft_slab * s, int a, int b);
+
+/* Speculative stage 1 (recompute path only): K1' = f(t_stage, XN) into A1, enqueued after stage 5
+   before the accept decision.  Accepted: swap K1 <-> A1 and skip the next stage 1; rejected: x and t
+   are unchanged, so K1 = f(t, x) is still exact and the next stage 1 is skipped as well (the
+   reference recomputes the identical K1).  pft_slab_eps_mark() before it lets eps_fetch() read
+   the error norm on a side stream while the speculative kernel runs. */
+int pft_slab_can_speculate(const pft_slab * s);
+int pft_slab_stage_spec(pft_slab * s, double t_stage, int k_begin, int k_end);
+int pft_slab_eps_mark(pft_slab * s);
 
 /* generic chunk-table combines for the host-staged path (any RK_MEM_DIST on a flat array) */
 int pft_flat_alloc(double ** p, size_t n);

@@ -33,7 +33,9 @@ enum {
 	PFT_OPT_KZ = 2,         /* planes per workgroup z-march; 0 (default) = automatic: one full
 	                           round of resident workgroups (pft_slab_set_kz) */
 	PFT_OPT_DEVICE = 3,     /* HIP device of this thread's slab (default: current device) */
-	PFT_OPT_TIMING = 4,     /* 1: time every stage with HIP events (stats.stage_ms) */
+	PFT_OPT_TIMING = 4,     /* N > 0: time the stages of every N-th attempted step with HIP events
+	                           (stats.stage_ms / stage_n); each timed stage adds ~3 us of
+	                           event-packet overhead, so benchmarks sample (N = 10) */
 	PFT_OPT_TILE = 5,       /* stage kernel: 1 (default) = per stage, 32 / 16 = LDS-tiled 64x8 /
 	                           32x16 tiles, 0 = cache-based kernel (pft_slab_set_tile) */
 	PFT_OPT_RECOMPUTE = 6   /* 1 (default): rebuild stage inputs from x and the K's inside the

@@ -29,6 +29,7 @@
 #pragma clang fp contract(off)
 
 #define PFT_BLOCK 256
+#define PFT_TRING 8
 
 // stage 5 of the recompute kernel keeps the combine operands of planes k and k+1 in registers
 // (measured 0.52 vs 0.65 ms at 400^3: re-loading them one plane later misses the 4 MiB L2)
@@ -882,6 +883,13 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu(STAGE
 // ------------------------------------------------------------------------------------------
 // layout conversion kernels (host padded layout, ghost thickness 2 <-> device layout)
 
+__global__ void publish_kernel(const unsigned long long* __restrict__ d, unsigned long long* host)
+{
+  host[0] = d[0];
+  host[1] = d[1];
+  __threadfence_system();
+}
+
 __global__ void pack_kernel(const double* __restrict__ host, double* __restrict__ dev, int n1, int n2,
                             int n3, long fs, long S)
 {
@@ -997,15 +1005,24 @@ struct pft_slab {
   long S;                // host padded block (one field)
   unsigned long long* scratch;  // [0] eps bits, [1] nonfinite flag
   unsigned long long* host_scratch;  // pinned
+  unsigned long long* host_pub;      // pinned, coherent: written by publish_kernel
+  unsigned long long* host_pub_dev;  // its device address
   hipStream_t stream, comm;
+  hipStream_t side;      // error-norm read-back while the compute stream runs ahead
+  hipEvent_t ev_eps;     // recorded on the compute stream after the error norm is final
+  int eps_marked;
   int kz;                // planes per workgroup z-march; 0 = automatic (one full round, see auto_kz)
   int n_cu;               // compute units of the slab's device
   double* noise;         // device u_noise (n3*plane) or null
   int tile_wx;           // 32 / 16: LDS-tiled kernels with that many threads per row; 1: per stage; 0: cache-based
   int n1_tiled_ok;
   int recompute;         // 1: stage inputs rebuilt from x and the K's (no aux arrays)
-  hipEvent_t tev[6][2];  // per-stage timing events
-  int tpending[6];
+  // per-stage timing: a ring of begin/end event pairs, so that kernels still running when the
+  // host collects (the speculative stage 1) are picked up by a later collect
+  hipEvent_t tev[6][PFT_TRING][2];
+  int thead[6], ttail[6];      // next slot to record / oldest slot not yet collected
+  double tacc_ms[6];           // collected but not yet handed out
+  long tacc_n[6];
 };
 
 extern "C" {
@@ -1052,8 +1069,12 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
   const size_t bytes = sizeof(double) * 3 * (size_t)s->fs;
   hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->comm, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&s->ev_eps, hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc((void**)&s->scratch, 64);
   if (e == hipSuccess) e = hipHostMalloc((void**)&s->host_scratch, 64, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&s->host_pub, 64, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&s->host_pub_dev, s->host_pub, 0);
   for (int b = 0; b < PFT_BUF_COUNT && e == hipSuccess; ++b) {
     e = hipMalloc((void**)&s->buf[b], bytes);
     // zero-fill on the slab's own stream: the compute stream is non-blocking, so a fill on the
@@ -1081,11 +1102,15 @@ int pft_slab_destroy(pft_slab* s)
   if (s->noise) (void)hipFree(s->noise);
   for (int st = 0; st < 6; ++st)
     for (int e = 0; e < 2; ++e)
-      if (s->tev[st][e]) (void)hipEventDestroy(s->tev[st][e]);
+      for (int r = 0; r < PFT_TRING; ++r)
+        if (s->tev[st][r][e]) (void)hipEventDestroy(s->tev[st][r][e]);
   if (s->scratch) (void)hipFree(s->scratch);
   if (s->host_scratch) (void)hipHostFree(s->host_scratch);
+  if (s->host_pub) (void)hipHostFree(s->host_pub);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   if (s->comm) (void)hipStreamDestroy(s->comm);
+  if (s->side) (void)hipStreamDestroy(s->side);
+  if (s->ev_eps) (void)hipEventDestroy(s->ev_eps);
   delete s;
   return 0;
 }
@@ -1325,7 +1350,7 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   a.h = h;
   // stage-input coefficients of the recompute path: exactly the solver's h/3.0, h/6.0, h/8.0, h
   a.cin = stage == 2 ? h / 3.0 : stage == 3 ? h / 6.0 : stage == 4 ? h / 8.0 : h;
-  if (kind == KFUSED && stage == 0) a.x = in;       // pure RHS: the input is the given buffer
+  if (kind == KFUSED && in) a.x = in;    // pure RHS / speculative stage 1: the input is the given buffer
   a.em0 = s->d.eps_mult[0];
   a.em1 = s->d.eps_mult[1];
   a.em2 = s->d.eps_mult[2];
@@ -1400,10 +1425,31 @@ int pft_slab_eps_reset(pft_slab* s)
   return 0;
 }
 
+int pft_slab_eps_mark(pft_slab* s)
+{
+  // the error norm goes to coherent pinned host memory by a one-thread kernel, and an event marks
+  // its completion: the host waits for that event only, never for a copy queued behind (or
+  // beside) the speculative stage-1 kernel that follows on the compute stream
+  publish_kernel<<<1, 1, 0, s->stream>>>(s->scratch, s->host_pub_dev);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(s->ev_eps, s->stream));
+  s->eps_marked = 1;
+  return 0;
+}
+
 int pft_slab_eps_fetch(pft_slab* s, double* eps, int* nonfinite)
 {
-  HIPCHK(hipMemcpyAsync(s->host_scratch, s->scratch, 16, hipMemcpyDeviceToHost, s->stream));
-  HIPCHK(hipStreamSynchronize(s->stream));
+  if (s->eps_marked) {
+    // read back on the side stream: work enqueued on the compute stream after the mark (the
+    // speculative stage 1 of the next step) keeps running while the host decides
+    s->eps_marked = 0;
+    HIPCHK(hipEventSynchronize(s->ev_eps));
+    s->host_scratch[0] = __atomic_load_n(&s->host_pub[0], __ATOMIC_ACQUIRE);
+    s->host_scratch[1] = __atomic_load_n(&s->host_pub[1], __ATOMIC_ACQUIRE);
+  } else {
+    HIPCHK(hipMemcpyAsync(s->host_scratch, s->scratch, 16, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+  }
   unsigned long long b = s->host_scratch[0];
   double v;
   memcpy(&v, &b, 8);
@@ -1412,29 +1458,86 @@ int pft_slab_eps_fetch(pft_slab* s, double* eps, int* nonfinite)
   return 0;
 }
 
+static int timing_collect(pft_slab* s, bool wait)
+{
+  for (int st = 1; st <= 5; ++st) {
+    while (s->ttail[st] < s->thead[st]) {
+      hipEvent_t* ev = s->tev[st][s->ttail[st] % PFT_TRING];
+      if (wait) {
+        HIPCHK(hipEventSynchronize(ev[1]));
+      } else {
+        const hipError_t q = hipEventQuery(ev[1]);
+        if (q == hipErrorNotReady) break;
+        if (q != hipSuccess) return fail(q, "hipEventQuery");
+      }
+      float e = 0.f;
+      HIPCHK(hipEventElapsedTime(&e, ev[0], ev[1]));
+      s->tacc_ms[st] += (double)e;
+      s->tacc_n[st] += 1;
+      s->ttail[st]++;
+    }
+  }
+  return 0;
+}
+
+static void timing_hand_out(pft_slab* s, double* ms, long* n)
+{
+  for (int st = 1; st <= 5; ++st) {
+    ms[st] += s->tacc_ms[st];
+    n[st] += s->tacc_n[st];
+    s->tacc_ms[st] = 0.0;
+    s->tacc_n[st] = 0;
+  }
+}
+
 int pft_slab_timing_mark(pft_slab* s, int stage, int end)
 {
   if (stage < 1 || stage > 5) return -2;
-  if (!s->tev[stage][0]) {
-    HIPCHK(hipEventCreate(&s->tev[stage][0]));
-    HIPCHK(hipEventCreate(&s->tev[stage][1]));
+  if (!end && s->thead[stage] - s->ttail[stage] >= PFT_TRING) {
+    int rc = timing_collect(s, true);   // ring full: read the oldest pairs before re-recording them
+    if (rc) return rc;
   }
-  HIPCHK(hipEventRecord(s->tev[stage][end ? 1 : 0], s->stream));
-  if (end) s->tpending[stage] = 1;
+  hipEvent_t* ev = s->tev[stage][s->thead[stage] % PFT_TRING];
+  if (!ev[0]) {
+    HIPCHK(hipEventCreate(&ev[0]));
+    HIPCHK(hipEventCreate(&ev[1]));
+  }
+  HIPCHK(hipEventRecord(ev[end ? 1 : 0], s->stream));
+  if (end) s->thead[stage]++;
   return 0;
 }
 
 int pft_slab_timing_collect(pft_slab* s, double* ms, long* n)
 {
-  for (int st = 1; st <= 5; ++st) {
-    if (!s->tpending[st]) continue;
-    float e = 0.f;
-    HIPCHK(hipEventSynchronize(s->tev[st][1]));
-    HIPCHK(hipEventElapsedTime(&e, s->tev[st][0], s->tev[st][1]));
-    ms[st] += (double)e;
-    n[st] += 1;
-    s->tpending[st] = 0;
-  }
+  int rc = timing_collect(s, false);
+  timing_hand_out(s, ms, n);
+  return rc;
+}
+
+int pft_slab_timing_flush(pft_slab* s, double* ms, long* n)
+{
+  int rc = timing_collect(s, true);
+  timing_hand_out(s, ms, n);
+  return rc;
+}
+
+int pft_slab_can_speculate(const pft_slab* s) { return slab_kind(s) == KFUSED; }
+
+int pft_slab_stage_spec(pft_slab* s, double t_stage, int k_begin, int k_end)
+{
+  // stage 1 of the next step, K1' = f(t + h, x(t + h)), from XN into A1 (unused on the recompute
+  // path) -- before the accept decision is known
+  if (slab_kind(s) != KFUSED) return -2;
+  return run_stage(s, 1, s->buf[PFT_BUF_XN], s->buf[PFT_BUF_A1], nullptr, t_stage, 0.0, 0.0, k_begin, k_end,
+                   s->d.gl_static, KFUSED);
+}
+
+int pft_slab_swap_buffers(pft_slab* s, int a, int b)
+{
+  if (a < 0 || a >= PFT_BUF_COUNT || b < 0 || b >= PFT_BUF_COUNT) return -2;
+  double* t = s->buf[a];
+  s->buf[a] = s->buf[b];
+  s->buf[b] = t;
   return 0;
 }
 

@@ -41,6 +41,7 @@ typedef struct {
 	double *h_k, *h_aux; int h_cap;
 	/* options */
 	int opt_gls, opt_kz, opt_dev, opt_timing, opt_tile, opt_norecompute;
+	int tstep;                  /* this attempted step's stages are timed (every opt_timing-th) */
 	pft_solver_stats stats;
 } solver_state;
 
@@ -119,7 +120,7 @@ int pft_solver_set_option(int opt, long value)
 		case PFT_OPT_GL_STATIC: R.opt_gls = value ? 1 : 0; return 0;
 		case PFT_OPT_KZ: if(value < 0) return -2; R.opt_kz = (int)value; if(R.slab) pft_slab_set_kz(R.slab, R.opt_kz); return 0;
 		case PFT_OPT_DEVICE: R.opt_dev = (int)value; return 0;
-		case PFT_OPT_TIMING: R.opt_timing = value ? 1 : 0; return 0;
+		case PFT_OPT_TIMING: if(value < 0) return -2; R.opt_timing = (int)value; return 0;
 		case PFT_OPT_RECOMPUTE:
 			R.opt_norecompute = value ? 0 : 1; if(R.slab) pft_slab_set_recompute(R.slab, !R.opt_norecompute); return 0;
 		case PFT_OPT_TILE:
@@ -192,25 +193,33 @@ static int canonical_chunks(const RK_MEM_DIST * n, double em[3])
 	return R.max_n >= PFT_VAR_COUNT*S;
 }
 
+/* one stage of the step on this slab; stage 6 = the speculative stage 1 of the next step
+   (K1' = f(ts, XN) into A1, pft_slab_stage_spec) */
+static int run1(int stage, double ts, double coef, double h, int kb, int ke)
+{
+	return stage == 6 ? pft_slab_stage_spec(R.slab, ts, kb, ke) : pft_slab_stage(R.slab, stage, ts, coef, h, kb, ke);
+}
+
 static int do_stage(int stage, double ts, double coef, double h, int nfields, long * launches)
 {
 	pft_comm * c = comm();
-	const int out_buf = pft_slab_stage_output(R.slab, stage);
+	const int out_buf = stage == 6 ? PFT_BUF_A1 : pft_slab_stage_output(R.slab, stage);
+	const int tstage = stage == 6 ? 1 : stage;
 	int rc, n3;
-	if(R.opt_timing) pft_slab_timing_mark(R.slab, stage, 0);
+	if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 0);
 	if(pft_comm_size(c) == 1) {
 		(*launches)++;
-		rc = pft_slab_stage(R.slab, stage, ts, coef, h, -1, -1);
-		if(R.opt_timing) pft_slab_timing_mark(R.slab, stage, 1);
+		rc = run1(stage, ts, coef, h, -1, -1);
+		if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
 		return rc;
 	}
 	/* boundary planes first, their exchange overlaps the interior sweep */
 	n3 = R.slab_grid.n3;
-	if((rc = pft_slab_stage(R.slab, stage, ts, coef, h, 0, 1))) return rc;
-	if(n3 > 1 && (rc = pft_slab_stage(R.slab, stage, ts, coef, h, n3-1, n3))) return rc;
+	if((rc = run1(stage, ts, coef, h, 0, 1))) return rc;
+	if(n3 > 1 && (rc = run1(stage, ts, coef, h, n3-1, n3))) return rc;
 	if((rc = pft_comm_halo_start(c, out_buf, 0, nfields))) return rc;
-	if(n3 > 2 && (rc = pft_slab_stage(R.slab, stage, ts, coef, h, 1, n3-1))) return rc;
-	if(R.opt_timing) pft_slab_timing_mark(R.slab, stage, 1);
+	if(n3 > 2 && (rc = run1(stage, ts, coef, h, 1, n3-1))) return rc;
+	if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
 	*launches += 3;
 	return pft_comm_halo_finish(c);
 }
@@ -231,6 +240,7 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	int nonfinite, rc, ret = 0;
 	long attempted = 0, launches = 0;
 	const int nf = R.opt_gls ? 2 : 3;     /* fields whose stage values change */
+	int spec, k1_valid = 0;               /* K1 holds f(t, x) for the current t and x */
 
 	if((rc = ensure_slab())) return rc;
 	pft_slab_set_eps_mult(R.slab, em);
@@ -244,17 +254,29 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	}
 	R.device_valid = 0;
 	R.stats.path = 1;
+	/* The next step's K1 is computed speculatively right after stage 5 (recompute path): the
+	   kernel runs while the host reads the error norm and decides, so the GPU does not idle
+	   between steps.  Accepted: it is f(t+h, x(t+h)), exactly the next stage 1.  Rejected: x and t
+	   are unchanged, so the current K1 is still exactly f(t, x) -- the reference recomputes the
+	   same bits (hybrid2.c:373) -- and the speculative one is dropped. */
+	spec = pft_slab_can_speculate(R.slab);
 
 	while(1) {
 		h2 = h/2.0; h3 = h/3.0; h6 = h/6.0; h8 = h/8.0;                          /* :355 */
+		R.tstep = R.opt_timing > 0 && attempted % R.opt_timing == 0;
 		if((rc = pft_slab_eps_reset(R.slab))) return rc;
 		/* K1 = f(t,x); aux = x + K1 h/3 ... K5 = f(t+h, aux); error norm; x(t+h) candidate */
-		if((rc = do_stage(1, t,    h3, h, nf, &launches))) return rc;    /* :373-389 */
+		if(!(spec && k1_valid) && (rc = do_stage(1, t, h3, h, nf, &launches))) return rc;  /* :373-389 */
+		k1_valid = 1;
 		if((rc = do_stage(2, t+h3, h6, h, nf, &launches))) return rc;    /* :392-409 */
 		if((rc = do_stage(3, t+h3, h8, h, nf, &launches))) return rc;    /* :412-429 */
 		if((rc = do_stage(4, t+h2, h,  h, nf, &launches))) return rc;    /* :432-450 */
 		if((rc = do_stage(5, t+h,  h3, h, nf, &launches))) return rc;    /* :453,507-524,657-668 */
 		if((rc = pft_comm_allreduce_eps(c))) return rc;                          /* :572 */
+		if(spec) {
+			if((rc = pft_slab_eps_mark(R.slab))) return rc;
+			if((rc = do_stage(6, t+h, 0.0, h, nf, &launches))) return rc;
+		}
 		if((rc = pft_slab_eps_fetch(R.slab, &eps, &nonfinite))) return rc;
 		if(R.opt_timing) pft_slab_timing_collect(R.slab, R.stats.stage_ms, R.stats.stage_n);
 		system->steps_total++;                                                   /* :460 */
@@ -281,6 +303,8 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 			if(command & RKA_CMD_UPDATE) {                                       /* :651-668 */
 				t += h;
 				pft_slab_accept(R.slab);
+				if(spec) pft_slab_swap_buffers(R.slab, PFT_BUF_K1, PFT_BUF_A1);  /* K1 = f(t, x) */
+				else k1_valid = 0;
 				system->steps++;
 				if(system->Service_Callback != NULL) {                           /* :676-685 */
 					system->t = t;
@@ -317,6 +341,8 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	}
 	(void)rank;
 	if(ret != 1 && ret != -4) system->t = t;                                     /* :768 */
+	if(R.opt_timing) pft_slab_timing_flush(R.slab, R.stats.stage_ms, R.stats.stage_n);
+	R.tstep = 0;
 	R.device_valid = 1;
 	R.stats.kernel_launches = launches;
 	R.stats.steps_total = attempted;

@@ -11,6 +11,6 @@ while read -r args; do
   for rep in $(seq ${REPS:-1}); do
     timeout -k 10 300 python bench.py --steps ${STEPS:-60} --warmup 5 --no-cpu $args > $OUT/c${i}_r${rep}.json 2>>$OUT/err.log
     rc=$?; [ $rc -ge 124 ] && exit $rc
-    python3 -c "import json,sys;d=json.load(open('$OUT/c${i}_r${rep}.json'));print('$args'.ljust(40), d['value'], d['ms_per_step'], d['roofline']['stages_ms'])"
+    python3 -c "import json,sys;d=json.load(open('$OUT/c${i}_r${rep}.json'));print('$args'.ljust(40), d['value'], d['ms_per_step'], (d['roofline'] or {}).get('stages_ms'))"
   done
 done <<< "$CONFIGS"
