@@ -69,7 +69,7 @@ def parse():
     ap.add_argument("--no-recompute", action="store_true",
                     help="materialise the reference's aux arrays between stages (72 vs 54 doubles/cell-step)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+    ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="CPU sample: attempted steps (in batches of 2) until this much time has passed")
     ap.add_argument("--no-timing", action="store_true", help="no HIP-event stage timing")
     ap.add_argument("--host-boundary", action="store_true",
@@ -305,7 +305,7 @@ def cpu_baseline(sim, base, a):
         return time.perf_counter() - t0
 
     run(1)                                           # first touch of the oracle's arrays (not counted)
-    per_step = run(2) / 2.0                          # sizes the sample (not counted)
+    per_step = run(3) / 3.0                          # sizes the sample (not counted)
     n = max(2, int(a.cpu_seconds / per_step))
     stt.value = 0
     el = run(n)

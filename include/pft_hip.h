@@ -128,8 +128,9 @@ int pft_slab_swap_buffers(pft_slab * s, int a, int b);
 /* Speculative stage 1 (recompute path only): K1' = f(t_stage, XN) into A1, enqueued after stage 5
    before the accept decision.  Accepted: swap K1 <-> A1 and skip the next stage 1; rejected: x and t
    are unchanged, so K1 = f(t, x) is still exact and the next stage 1 is skipped as well (the
-   reference recomputes the identical K1).  pft_slab_eps_mark() before it lets eps_fetch() read
-   the error norm on a side stream while the speculative kernel runs. */
+   reference recomputes the identical K1).  pft_slab_eps_mark() before it publishes the error norm
+   to pinned host memory (and resets it for the next step), so that eps_fetch() returns while the
+   speculative kernel runs. */
 int pft_slab_can_speculate(const pft_slab * s);
 int pft_slab_stage_spec(pft_slab * s, double t_stage, int k_begin, int k_end);
 int pft_slab_eps_mark(pft_slab * s);

@@ -883,10 +883,12 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu(STAGE
 // ------------------------------------------------------------------------------------------
 // layout conversion kernels (host padded layout, ghost thickness 2 <-> device layout)
 
-__global__ void publish_kernel(const unsigned long long* __restrict__ d, unsigned long long* host)
+__global__ void publish_kernel(unsigned long long* __restrict__ d, unsigned long long* host)
 {
   host[0] = d[0];
   host[1] = d[1];
+  d[0] = 0;              // ready for the next step's error norm (no separate fill)
+  d[1] = 0;
   __threadfence_system();
 }
 
@@ -1427,9 +1429,10 @@ int pft_slab_eps_reset(pft_slab* s)
 
 int pft_slab_eps_mark(pft_slab* s)
 {
-  // the error norm goes to coherent pinned host memory by a one-thread kernel, and an event marks
-  // its completion: the host waits for that event only, never for a copy queued behind (or
-  // beside) the speculative stage-1 kernel that follows on the compute stream
+  // the error norm goes to coherent pinned host memory by a one-thread kernel (which also resets
+  // it for the next step), and an event marks its completion: the host waits for that event
+  // only, never for a copy queued behind (or beside) the speculative stage-1 kernel that follows
+  // on the compute stream
   publish_kernel<<<1, 1, 0, s->stream>>>(s->scratch, s->host_pub_dev);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(s->ev_eps, s->stream));

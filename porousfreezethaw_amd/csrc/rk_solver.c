@@ -264,7 +264,8 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	while(1) {
 		h2 = h/2.0; h3 = h/3.0; h6 = h/6.0; h8 = h/8.0;                          /* :355 */
 		R.tstep = R.opt_timing > 0 && attempted % R.opt_timing == 0;
-		if((rc = pft_slab_eps_reset(R.slab))) return rc;
+		/* the error norm accumulator is reset by its publication on the speculative path */
+		if((!spec || attempted == 0) && (rc = pft_slab_eps_reset(R.slab))) return rc;
 		/* K1 = f(t,x); aux = x + K1 h/3 ... K5 = f(t+h, aux); error norm; x(t+h) candidate */
 		if(!(spec && k1_valid) && (rc = do_stage(1, t, h3, h, nf, &launches))) return rc;  /* :373-389 */
 		k1_valid = 1;
