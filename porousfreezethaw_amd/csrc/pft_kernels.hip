@@ -38,6 +38,9 @@
 #endif
 // minimum waves per SIMD of the fused stage kernels 1-4 (stage 5 keeps ~250 VGPRs live: capped
 // at 256 so that two waves fit)
+#ifndef PFT_DEEP_MASK
+#define PFT_DEEP_MASK ((1 << 3) | (1 << 4))   // stages with the two-deep z pipeline
+#endif
 #ifndef PFT_FUSED_WAVES
 #define PFT_FUSED_WAVES 3
 #endif
@@ -664,7 +667,7 @@ __device__ __forceinline__ void keep5(int q, const Ops& r, dbl2& x, dbl2& k1, db
 }
 
 template <int STAGE, int MODE, bool GLS, int WX>
-__global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu(STAGE == 5 ? 2 : PFT_FUSED_WAVES))) void merson_fused(StageArgs a, pft_consts c)
+__global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((STAGE == 5 || (GLS && ((PFT_DEEP_MASK >> STAGE) & 1))) ? 2 : PFT_FUSED_WAVES))) void merson_fused(StageArgs a, pft_consts c)
 {
   using G = TileGeo<WX>;
   __shared__ __attribute__((aligned(16))) double lds[2][3][G::LF];
@@ -700,6 +703,13 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu(STAGE
   // face reuse (rhs_cell_f) in stages 1-4; stage 5 already holds ~250 VGPRs of combine operands
   // and the z-face carry would push it past 256 (one wave per SIMD): measured 0.58 vs 0.53 ms
   constexpr bool FACE = STAGE != 5;
+  // two-deep z pipeline (stages in PFT_DEEP_MASK, gl_static builds): the raw operands of plane k+2
+  // are loaded while plane k is computed (the stage input of plane k+1 is its z+1 neighbour, so a
+  // one-deep pipeline waits for its loads before the stencil).  It costs the operand registers:
+  // 198 VGPRs = 2 waves/SIMD for stages 3-4.  Measured at 400^3: gl_static stages 3-4 0.275 vs
+  // 0.294 ms; faithful (3 evolving fields, more operands) 0.376 vs 0.370 -- kept off there.
+  constexpr bool DEEP = GLS && ((PFT_DEEP_MASK >> STAGE) & 1) != 0 && STAGE >= 1 && STAGE <= 4;
+  Ops pn[3], ph;                       // DEEP: operands of plane k+1 (centre, halo pair)
   FaceT fz[2];                         // z-face below plane k of each cell of the pair
 #ifdef PFT_S5_KEEP
   // stage 5 keeps x, K1, K4 and the K1/K3/K4 part of the error norm of planes k and k+1
@@ -730,6 +740,13 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu(STAGE
       load_ops<STAGE, GLS>(a, hf, (long)(kb + 1) * a.plane + hp, tmp);
       st2(&lds[0][hf][hl], stage_in<STAGE, GLS>(a, hf, tmp));
     }
+    if constexpr (DEEP) {
+      if (!((kb == a.n3 - 1) && !a.has_above)) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) load_ops<STAGE, GLS>(a, q, o0 + a.plane, pn[q]);
+      }
+      if (hact && kb + 1 < ke) load_ops<STAGE, GLS>(a, hf, (long)(kb + 2) * a.plane + hp, ph);
+    }
     // the z-face below the chunk's first plane; later planes inherit it from the plane below
     if constexpr (FACE) {
 #pragma unroll
@@ -746,12 +763,16 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu(STAGE
     if (!top) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
-        Ops nop;
-        load_ops<STAGE, GLS>(a, q, o + a.plane, nop);
-        zp[q] = stage_in<STAGE, GLS>(a, q, nop);
+        if constexpr (DEEP) {
+          zp[q] = stage_in<STAGE, GLS>(a, q, pn[q]);
+        } else {
+          Ops nop;
+          load_ops<STAGE, GLS>(a, q, o + a.plane, nop);
+          zp[q] = stage_in<STAGE, GLS>(a, q, nop);
 #ifdef PFT_S5_KEEP
-        if (STAGE == 5) keep5<GLS>(q, nop, nx[q], nk1[q], nk4[q], nE[q]);
+          if (STAGE == 5) keep5<GLS>(q, nop, nx[q], nk1[q], nk4[q], nE[q]);
 #endif
+        }
       }
     }
     dbl2 hv = {0.0, 0.0};
@@ -759,9 +780,23 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu(STAGE
 #pragma unroll
       for (int q = 0; q < 3; ++q) st2(&lds[cur ^ 1][q][lo], zp[q]);
       if (hact) {
-        Ops tmp;
-        load_ops<STAGE, GLS>(a, hf, (long)(k + 2) * a.plane + hp, tmp);
-        hv = stage_in<STAGE, GLS>(a, hf, tmp);
+        if constexpr (DEEP) {
+          hv = stage_in<STAGE, GLS>(a, hf, ph);
+        } else {
+          Ops tmp;
+          load_ops<STAGE, GLS>(a, hf, (long)(k + 2) * a.plane + hp, tmp);
+          hv = stage_in<STAGE, GLS>(a, hf, tmp);
+        }
+      }
+    }
+    if constexpr (DEEP) {
+      // operands of plane k+2 (and its halo pair), in flight during the stencil of plane k
+      if (more) {
+        if (!((k + 1 == a.n3 - 1) && !a.has_above)) {
+#pragma unroll
+          for (int q = 0; q < 3; ++q) load_ops<STAGE, GLS>(a, q, o + 2 * a.plane, pn[q]);
+        }
+        if (hact && k + 2 < ke) load_ops<STAGE, GLS>(a, hf, (long)(k + 3) * a.plane + hp, ph);
       }
     }
     double du[2], dp[2];
