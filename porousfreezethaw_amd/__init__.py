@@ -64,6 +64,13 @@ class pft_grid(C.Structure):
                 ("L1", C.c_double), ("L2", C.c_double), ("L3", C.c_double), ("calc_mode", C.c_int)]
 
 
+class pft_snapshot_info(C.Structure):
+    """include/pft_io.h: the attributes of a snapshot dataset (intertrack.c:2393-2406)"""
+    _fields_ = [("t", C.c_double), ("tau", C.c_double), ("final_time", C.c_double), ("delta", C.c_double),
+                ("snapshot", C.c_int), ("total_snapshots", C.c_int), ("calc_mode", C.c_int),
+                ("title", C.c_char * 256), ("L1", C.c_double), ("L2", C.c_double), ("L3", C.c_double)]
+
+
 class pft_solver_stats(C.Structure):
     _fields_ = [("path", C.c_int), ("nprocs", C.c_int), ("rank", C.c_int),
                 ("kernel_launches", C.c_long), ("steps_total", C.c_long), ("last_eps", C.c_double),
@@ -129,6 +136,13 @@ def lib():
         L.pft_slab_stream.argtypes = [C.c_void_p]
         L.pft_slab_stream.restype = C.c_void_p
         L.pft_hip_device_sync.restype = C.c_int
+        gp, sp = C.POINTER(pft_grid), C.POINTER(pft_snapshot_info)
+        L.pft_snapshot_create.argtypes = [C.c_char_p, gp, dp, sp, C.c_int]
+        L.pft_snapshot_write_slab.argtypes = [C.c_char_p, gp, dp]
+        L.pft_snapshot_write.argtypes = [C.c_char_p, gp, dp, sp, dp]
+        L.pft_snapshot_read_info.argtypes = [C.c_char_p, ip, ip, ip, sp, dp]
+        L.pft_snapshot_read_slab.argtypes = [C.c_char_p, gp, dp]
+        L.pft_snapshot_title.argtypes = [C.c_char_p, C.c_int, C.c_char_p, C.c_double]
         _lib = L
     return _lib
 
@@ -275,6 +289,39 @@ class Simulation:
             self.lib.RK_MPI_SA_cleanup()
             self.initialised = False
         self.lib.FreePrecalcData()
+
+
+def snapshot_info(t, tau, final_time, delta, calc_mode, snapshot=0, total_snapshots=0, comment=""):
+    """pft_snapshot_info; its title is the reference's "Intertrack simulation (<comment>). Time: <t>"."""
+    info = pft_snapshot_info(t, tau, final_time, delta, snapshot, total_snapshots, calc_mode)
+    info.title = ("Intertrack simulation (%s). Time: %g" % (comment, t)).encode()[:255]   # C's %g
+    return info
+
+
+def save_snapshot(sim, path, info):
+    """Write this slab's part of a NetCDF-classic snapshot (pft_io.h); the host array must hold the
+    state (Simulation.download() after a device-resident solve).  Multi-rank: every rank calls it."""
+    rc = lib().pft_snapshot_write(os.fsencode(path), C.byref(sim.grid), _dp(sim.params), C.byref(info), _dp(sim.x))
+    if rc:
+        raise OSError(f"pft_snapshot_write({path}) failed ({rc})")
+
+
+def read_snapshot_info(path):
+    """(n1, n2, total_n3, pft_snapshot_info, params[PFT_PARAM_COUNT]) of a snapshot dataset"""
+    n1, n2, n3 = C.c_int(), C.c_int(), C.c_int()
+    info = pft_snapshot_info()
+    prm = np.full(len(PARAM_NAMES), np.nan)
+    rc = lib().pft_snapshot_read_info(os.fsencode(path), C.byref(n1), C.byref(n2), C.byref(n3), C.byref(info), _dp(prm))
+    if rc:
+        raise OSError(f"pft_snapshot_read_info({path}) failed ({rc})")
+    return n1.value, n2.value, n3.value, info, prm
+
+
+def load_snapshot(sim, path):
+    """Fill this slab's interior from a snapshot dataset (restart / icond_file, intertrack.c:2040-2069)"""
+    rc = lib().pft_snapshot_read_slab(os.fsencode(path), C.byref(sim.grid), _dp(sim.x))
+    if rc:
+        raise OSError(f"pft_snapshot_read_slab({path}) failed ({rc})")
 
 
 def rhs(sim, t, state_padded=None):

@@ -321,3 +321,30 @@ def test_full_size_400_bitwise_and_rank_invariant():
     for r in range(2):
         assert out[r][0] == got
     assert np.array_equal(np.concatenate([out[0][1], out[1][1]], axis=1), x1)
+
+
+def test_snapshot_restart_continues_trajectory(tmp_path):
+    """continue_series (intertrack.c:1584-1669): a snapshot written at t = 36 s and read back into
+    a fresh solver (t, tau and the parameters from the dataset) continues the reference's
+    trajectory bit for bit to t = 360 s"""
+    meta, A = O.load_case("g20")
+    sim, Pm, info = make_sim(meta, A["traj_m0_ic"], mode=0)
+    T0, T1 = meta["traj_times"][:2]
+    sim.solve(T0)
+    path = str(tmp_path / "image.001.000.ncd")
+    P.save_snapshot(sim, path, P.snapshot_info(t=sim.t, tau=sim.h, final_time=T1, delta=info["delta"], calc_mode=0,
+                                               snapshot=1, total_snapshots=10, comment="restart test"))
+    s0, st0 = sim.system.steps, sim.system.steps_total
+    sim.close()
+    n1, n2, n3, inf, prm = P.read_snapshot_info(path)
+    assert (inf.L1, inf.L2, inf.L3) == (info["L1"], info["L2"], info["L3"])
+    sim2 = P.Simulation(n1, n2, n3, (inf.L1, inf.L2, inf.L3), inf.calc_mode, prm,
+                        initial=np.zeros((3, n3, n2, n1)), tau=inf.tau, t0=inf.t, tau_min=info["tau_min"],
+                        delta=inf.delta)
+    P.load_snapshot(sim2, path)
+    sim2.solve(inf.final_time)
+    ref = meta["traj_m0"][1]
+    assert (sim2.t, sim2.h, s0 + sim2.system.steps, st0 + sim2.system.steps_total) == \
+        (float.fromhex(ref[0]), float.fromhex(ref[1]), ref[2], ref[3])
+    assert np.array_equal(sim2.interior(), A["traj_m0_state1"])
+    sim2.close()
