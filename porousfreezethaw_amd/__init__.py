@@ -137,6 +137,7 @@ def lib():
         L.pft_slab_stream.restype = C.c_void_p
         L.pft_hip_device_sync.restype = C.c_int
         gp, sp = C.POINTER(pft_grid), C.POINTER(pft_snapshot_info)
+        L.pft_ic_eval.argtypes = [gp, C.c_int, C.c_int, ip, dp, dp]
         L.pft_snapshot_create.argtypes = [C.c_char_p, gp, dp, sp, C.c_int]
         L.pft_snapshot_write_slab.argtypes = [C.c_char_p, gp, dp]
         L.pft_snapshot_write.argtypes = [C.c_char_p, gp, dp, sp, dp]
@@ -185,7 +186,7 @@ class Simulation:
 
     def __init__(self, n1, n2, total_n3, L, calc_mode, params, nprocs=1, rank=0, beads=None,
                  initial=None, tau=1.0, tau_min=0.0, delta=1e-3, t0=0.0, gl_static=False, kz=None,
-                 init_solver=True, tile=None, recompute=True):
+                 init_solver=True, tile=None, recompute=True, icond=None):
         L1, L2, L3 = L
         self.lib = L_ = lib()
         self.grid = pft_grid()
@@ -199,7 +200,15 @@ class Simulation:
         self.N = (g.n3 + 4, g.n2 + 4, g.n1 + 4)
         self.S = int(np.prod(self.N))
         self.x = np.zeros(3 * self.S)
-        if initial is None:
+        if icond is not None:
+            # the parameter file's icond formulas, compiled by frontend.py (intertrack.c:1831-2012)
+            for q, prog in icond:
+                ops = np.array([o for o, _ in prog], dtype=np.int32)
+                args = np.array([a for _, a in prog], dtype=np.float64)
+                rc = L_.pft_ic_eval(C.byref(self.grid), q, len(prog), _ip(ops), _dp(args), _dp(self.x))
+                if rc:
+                    raise ValueError(f"pft_ic_eval failed ({rc})")
+        elif initial is None:
             L_.pft_model_ic_default(_dp(self.x))
         else:
             self.set_interior(initial)
@@ -221,7 +230,7 @@ class Simulation:
         self.initialised = False
         if L_.AllocPrecalcData():
             raise RuntimeError("AllocPrecalcData failed")
-        if beads is not None and initial is None:
+        if beads is not None and initial is None:   # (also after icond formulas)
             b = np.ascontiguousarray(beads, dtype=np.float64)
             L_.pft_model_set_beads(_dp(b), b.shape[0])
             L_.pft_model_set_solution(_dp(self.x))
