@@ -38,6 +38,11 @@
 #endif
 // minimum waves per SIMD of the fused stage kernels 1-4 (stage 5 keeps ~250 VGPRs live: capped
 // at 256 so that two waves fit)
+#ifdef PFT_S5_KEEP
+#define PFT_S5_WAVES2 1   // stage 5 keeps two planes of combine operands: 2 waves per SIMD
+#else
+#define PFT_S5_WAVES2 0
+#endif
 #ifndef PFT_DEEP_MASK
 #define PFT_DEEP_MASK ((1 << 3) | (1 << 4))   // stages with the two-deep z pipeline
 #endif
@@ -667,7 +672,7 @@ __device__ __forceinline__ void keep5(int q, const Ops& r, dbl2& x, dbl2& k1, db
 }
 
 template <int STAGE, int MODE, bool GLS, int WX>
-__global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((STAGE == 5 || (GLS && ((PFT_DEEP_MASK >> STAGE) & 1))) ? 2 : PFT_FUSED_WAVES))) void merson_fused(StageArgs a, pft_consts c)
+__global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_S5_WAVES2 && STAGE == 5) || (GLS && ((PFT_DEEP_MASK >> STAGE) & 1)) ? 2 : PFT_FUSED_WAVES))) void merson_fused(StageArgs a, pft_consts c)
 {
   using G = TileGeo<WX>;
   __shared__ __attribute__((aligned(16))) double lds[2][3][G::LF];
