@@ -1312,6 +1312,10 @@ extern "C" {
 static int slab_kind(const pft_slab* s)
 {
   if (s->d.n1 % 2 != 0 || s->tile_wx == 0) return KCACHE;   // 16-byte rows need n1 even
+  // automatic choice: a slab too small to fill the GPU with 512-cell tiles even one plane deep is
+  // latency-bound, and the cache kernel's 256-cell workgroups without LDS staging finish sooner
+  // (measured: 100^3, 250 k cells: 4 300 vs 3 700 Mcells*steps/s; 200^3, 2 M cells: 7 760 vs 9 040)
+  if (s->tile_wx == 1 && (long)s->plane * s->d.n3 < 4L * s->n_cu * 3 * 512) return KCACHE;
   return s->recompute ? KFUSED : KTILE;
 }
 
