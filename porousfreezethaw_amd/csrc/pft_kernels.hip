@@ -43,6 +43,9 @@
 #else
 #define PFT_S5_WAVES2 0
 #endif
+#ifndef PFT_S5_FACE
+#define PFT_S5_FACE 0
+#endif
 #ifndef PFT_DEEP_MASK
 #define PFT_DEEP_MASK ((1 << 3) | (1 << 4))   // stages with the two-deep z pipeline
 #endif
@@ -697,17 +700,25 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
   else if (h < G::LW) { hr = G::LH - 1; hcp = h - G::LW / 2; }
   else { const int q = h - G::LW; hr = 1 + q / 2; hcp = (q & 1) ? G::LW / 2 - 1 : 0; }
   const int hi = x0 - 2 + 2 * hcp, hj = y0 + hr - 1;
-  const bool hin = hi >= 0 && hi < a.n1 && hj >= 0 && hj < a.n2;
-  const long hp = hin ? (long)hj * a.n1 + hi : po;
+  // Walls in LDS: a halo pair outside the domain holds the mirror image the reference's ghost
+  // fill puts there (equation.c:137-174: ghost -1-m = interior m), so the stencil reads its x/y
+  // neighbours without selects.  Pair (-2,-1) = (v1, v0): pair (0,1) swapped; pair (n1, n1+1) =
+  // (v[n1-1], v[n1-2]): pair (n1-2, n1-1) swapped; rows -1 / n2 = rows 0 / n2-1.
+  const bool hswap = hi < 0 || hi >= a.n1;
+  const long hp = (long)(hj < 0 ? 0 : (hj >= a.n2 ? a.n2 - 1 : hj)) * a.n1 +
+                  (hi < 0 ? 0 : (hi >= a.n1 ? a.n1 - 2 : hi));
   const int hl = hr * G::LW + 2 * hcp;
+  // an inactive pair just right of the domain (partial tile) is the mirror of the last pair
+  const bool cswap = i0 == a.n1;
 
   double m = 0.0;
   bool nf = false;
   dbl2 zm[3], zc[3], zp[3];
   constexpr bool FLUX = MODE != 10 && MODE != 11;
   // face reuse (rhs_cell_f) in stages 1-4; stage 5 already holds ~250 VGPRs of combine operands
-  // and the z-face carry would push it past 256 (one wave per SIMD): measured 0.58 vs 0.53 ms
-  constexpr bool FACE = STAGE != 5;
+  // and the z-face carry spills there (measured 0.505 vs 0.470 ms) -- except with gl_static,
+  // whose fewer operands leave room (0.389 vs 0.415 ms)
+  constexpr bool FACE = STAGE != 5 || GLS || PFT_S5_FACE;
   // two-deep z pipeline (stages in PFT_DEEP_MASK, gl_static builds): the raw operands of plane k+2
   // are loaded while plane k is computed (the stage input of plane k+1 is its z+1 neighbour, so a
   // one-deep pipeline waits for its loads before the stencil).  It costs the operand registers:
@@ -738,12 +749,13 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
         load_ops<STAGE, GLS>(a, q, o0 - a.plane, tmp);  // plane below (exchanged ghost at kb == 0)
         zm[q] = stage_in<STAGE, GLS>(a, q, tmp);
       }
-      st2(&lds[0][q][lo], zc[q]);
+      st2(&lds[0][q][lo], cswap ? zc[q].yx : zc[q]);
     }
     if (hact) {
       Ops tmp;
       load_ops<STAGE, GLS>(a, hf, (long)(kb + 1) * a.plane + hp, tmp);
-      st2(&lds[0][hf][hl], stage_in<STAGE, GLS>(a, hf, tmp));
+      const dbl2 v = stage_in<STAGE, GLS>(a, hf, tmp);
+      st2(&lds[0][hf][hl], hswap ? v.yx : v);
     }
     if constexpr (DEEP) {
       if (!((kb == a.n3 - 1) && !a.has_above)) {
@@ -783,7 +795,7 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
     dbl2 hv = {0.0, 0.0};
     if (more) {
 #pragma unroll
-      for (int q = 0; q < 3; ++q) st2(&lds[cur ^ 1][q][lo], zp[q]);
+      for (int q = 0; q < 3; ++q) st2(&lds[cur ^ 1][q][lo], cswap ? zp[q].yx : zp[q]);
       if (hact) {
         if constexpr (DEEP) {
           hv = stage_in<STAGE, GLS>(a, hf, ph);
@@ -814,22 +826,11 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
         const double* L = lds[cur][q];
         const double cen = zc[q][s];
         col[q].c = cen;
-        if constexpr (FACE) {
-          // every LDS address is inside the tile's halo ring: load unconditionally, select the
-          // wall mirror (equation.c:164-174) without branching
-          const double lx = s == 0 ? L[lo - 1] : L[lo + 2];
-          const double ly0 = L[lo - G::LW + s], ly1 = L[lo + G::LW + s];
-          col[q].xm = s == 0 ? (i0 > 0 ? lx : cen) : zc[q][0];
-          col[q].xp = s == 0 ? zc[q][1] : (i0 + 2 < a.n1 ? lx : cen);
-          col[q].ym = j > 0 ? ly0 : cen;
-          col[q].yp = j < a.n2 - 1 ? ly1 : cen;
-        } else {
-          // (stage 5: the branchy form needs fewer live registers)
-          col[q].xm = s == 0 ? (i0 > 0 ? L[lo - 1] : cen) : zc[q][0];
-          col[q].xp = s == 0 ? zc[q][1] : (i0 + 2 < a.n1 ? L[lo + 2] : cen);
-          col[q].ym = j > 0 ? L[lo - G::LW + s] : cen;
-          col[q].yp = j < a.n2 - 1 ? L[lo + G::LW + s] : cen;
-        }
+        // x/y neighbours straight from LDS: the walls' mirror values are in the halo
+        col[q].xm = s == 0 ? L[lo - 1] : zc[q][0];
+        col[q].xp = s == 0 ? zc[q][1] : L[lo + 2];
+        col[q].ym = L[lo - G::LW + s];
+        col[q].yp = L[lo + G::LW + s];
         col[q].zm = zm[q][s];
         col[q].zp = top ? cen : zp[q][s];
       }
@@ -845,7 +846,7 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
         rhs_cell<MODE>(c, col[0], col[1], col[2], un, du[s], dp[s]);
       }
     }
-    if (more && hact) st2(&lds[cur ^ 1][hf][hl], hv);
+    if (more && hact) st2(&lds[cur ^ 1][hf][hl], hswap ? hv.yx : hv);
     if (active) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
