@@ -43,6 +43,9 @@
 #else
 #define PFT_S5_WAVES2 0
 #endif
+#ifndef PFT_S5_GLZERO
+#define PFT_S5_GLZERO 1
+#endif
 #ifndef PFT_S5_FACE
 #define PFT_S5_FACE 0
 #endif
@@ -667,7 +670,7 @@ template <bool GLS>
 __device__ __forceinline__ void keep5(int q, const Ops& r, dbl2& x, dbl2& k1, dbl2& k4, dbl2& E)
 {
   x = r.x;
-  if (GLS && q == 2) return;
+  if ((GLS || PFT_S5_GLZERO) && q == 2) return;
   k1 = r.k1;
   k4 = r.k4;
 #pragma unroll
@@ -859,7 +862,16 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
           // operands of plane k again (loaded one iteration ago: an L2 hit; keeping them in
           // registers as well would double the stage-5 register file and halve occupancy)
 #ifdef PFT_S5_KEEP
-          const dbl2 ox = cx[q], ok1 = ck1[q], ok4 = ck4[q], oE = cE[q];
+          // gl (q = 2): K1, K4 and the K part of the error norm are the exact zeros the stages
+          // stored for dgl (equation.c:731), so they are not carried in registers
+          constexpr dbl2 zero2 = {0.0, 0.0};
+          const bool z2 = PFT_S5_GLZERO && q == 2;
+          const dbl2 ox = cx[q], ok1 = z2 ? zero2 : ck1[q], ok4 = z2 ? zero2 : ck4[q];
+          dbl2 oE = cE[q];
+          if (z2) {
+#pragma unroll
+            for (int s = 0; s < 2; ++s) oE[s] = 0.2 * 0.0 - 0.9 * 0.0 + 0.8 * 0.0;   // :521 prefix
+          }
 #else
           Ops op;
           load_ops<STAGE, GLS>(a, q, o, op);
