@@ -456,6 +456,12 @@ struct TileGeo {
 
 __device__ __forceinline__ dbl2 ld2(const double* p) { return *reinterpret_cast<const dbl2*>(p); }
 __device__ __forceinline__ void st2(double* p, dbl2 v) { *reinterpret_cast<dbl2*>(p) = v; }
+// store a pair with its halves exchanged when sw = 1 (two 8-byte stores at per-thread offsets)
+__device__ __forceinline__ void st2x(double* p, dbl2 v, int sw)
+{
+  p[sw] = v.x;
+  p[1 - sw] = v.y;
+}
 
 template <int STAGE, int MODE, bool GLS, int WX>
 __global__ __launch_bounds__(PFT_BLOCK) void merson_tile(StageArgs a, pft_consts c)
@@ -711,8 +717,11 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
   const long hp = (long)(hj < 0 ? 0 : (hj >= a.n2 ? a.n2 - 1 : hj)) * a.n1 +
                   (hi < 0 ? 0 : (hi >= a.n1 ? a.n1 - 2 : hi));
   const int hl = hr * G::LW + 2 * hcp;
-  // an inactive pair just right of the domain (partial tile) is the mirror of the last pair
+  // an inactive pair just right of the domain (partial tile) is the mirror of the last pair.
+  // Swapped pairs are stored as two 8-byte halves at exchanged offsets (per-thread constants),
+  // not through per-store selects.
   const bool cswap = i0 == a.n1;
+  const int c0 = cswap ? 1 : 0, h0 = hswap ? 1 : 0;
 
   double m = 0.0;
   bool nf = false;
@@ -752,13 +761,13 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
         load_ops<STAGE, GLS>(a, q, o0 - a.plane, tmp);  // plane below (exchanged ghost at kb == 0)
         zm[q] = stage_in<STAGE, GLS>(a, q, tmp);
       }
-      st2(&lds[0][q][lo], cswap ? zc[q].yx : zc[q]);
+      st2x(&lds[0][q][lo], zc[q], c0);
     }
     if (hact) {
       Ops tmp;
       load_ops<STAGE, GLS>(a, hf, (long)(kb + 1) * a.plane + hp, tmp);
       const dbl2 v = stage_in<STAGE, GLS>(a, hf, tmp);
-      st2(&lds[0][hf][hl], hswap ? v.yx : v);
+      st2x(&lds[0][hf][hl], v, h0);
     }
     if constexpr (DEEP) {
       if (!((kb == a.n3 - 1) && !a.has_above)) {
@@ -798,7 +807,7 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
     dbl2 hv = {0.0, 0.0};
     if (more) {
 #pragma unroll
-      for (int q = 0; q < 3; ++q) st2(&lds[cur ^ 1][q][lo], cswap ? zp[q].yx : zp[q]);
+      for (int q = 0; q < 3; ++q) st2x(&lds[cur ^ 1][q][lo], zp[q], c0);
       if (hact) {
         if constexpr (DEEP) {
           hv = stage_in<STAGE, GLS>(a, hf, ph);
@@ -819,6 +828,11 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
         if (hact && k + 2 < ke) load_ops<STAGE, GLS>(a, hf, (long)(k + 3) * a.plane + hp, ph);
       }
     }
+    if (top) {                         // top wall (uniform): mirror p, gl; Dirichlet u (equation.c:175-183)
+#pragma unroll
+      for (int q = 1; q < 3; ++q) zp[q] = zc[q];
+      zp[0] = dbl2{a.T_top, a.T_top};
+    }
     double du[2], dp[2];
     FaceT fx;                          // the x-face between the pair's two cells
 #pragma unroll
@@ -835,9 +849,8 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
         col[q].ym = L[lo - G::LW + s];
         col[q].yp = L[lo + G::LW + s];
         col[q].zm = zm[q][s];
-        col[q].zp = top ? cen : zp[q][s];
+        col[q].zp = zp[q][s];
       }
-      if (top) col[0].zp = a.T_top;
       const double un = a.noise ? zc[0][s] + a.noise[(long)k * a.plane + po + s] : zc[0][s];
       if constexpr (FACE) {
         const FaceT fxm =
@@ -849,7 +862,7 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
         rhs_cell<MODE>(c, col[0], col[1], col[2], un, du[s], dp[s]);
       }
     }
-    if (more && hact) st2(&lds[cur ^ 1][hf][hl], hswap ? hv.yx : hv);
+    if (more && hact) st2x(&lds[cur ^ 1][hf][hl], hv, h0);
     if (active) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
