@@ -80,6 +80,11 @@ int pft_model_set_beads(const double * beads, int nbeads);
 int pft_model_load_beads(const char * path);             /* same file format as the reference */
 int PrecalculateData(FLOAT * var_eps_mult);              /* overlays beads on the configured solution */
 int pft_model_set_solution(FLOAT * solution);            /* the driver's `solution` array */
+/* the slab's u_noise field (equation.c:450-456: u_noise_amp*(rand()/RAND_MAX - 0.5) per interior
+   node, [k][j][i]); NULL when u_noise_amp == 0.  The reference seeds rand() with the time
+   (intertrack.c:1278), so its noise is not reproducible; libpft draws from the process's rand()
+   stream as it stands (srand() before PrecalculateData to fix it). */
+const FLOAT * pft_model_noise(void);
 
 /* Right-hand sides with the reference signature (RK_RightHandSide).  Called on HOST arrays they
    run the device kernels on a staged copy; the solver recognises them and runs its fused

@@ -138,6 +138,7 @@ def lib():
         L.pft_hip_device_sync.restype = C.c_int
         gp, sp = C.POINTER(pft_grid), C.POINTER(pft_snapshot_info)
         L.pft_ic_eval.argtypes = [gp, C.c_int, C.c_int, ip, dp, dp]
+        L.pft_model_noise.restype = dp
         L.pft_snapshot_create.argtypes = [C.c_char_p, gp, dp, sp, C.c_int]
         L.pft_snapshot_write_slab.argtypes = [C.c_char_p, gp, dp]
         L.pft_snapshot_write.argtypes = [C.c_char_p, gp, dp, sp, dp]

@@ -348,3 +348,30 @@ def test_snapshot_restart_continues_trajectory(tmp_path):
         (float.fromhex(ref[0]), float.fromhex(ref[1]), ref[2], ref[3])
     assert np.array_equal(sim2.interior(), A["traj_m0_state1"])
     sim2.close()
+
+
+@pytest.mark.parametrize("mode", [0, 1, 10, 11])
+@pytest.mark.parametrize("flavour", ["default", "fused32", "tile16", "cache"])
+def test_rhs_with_temperature_noise(mode, flavour):
+    """u_noise (u_noise_amp != 0, equation.c:450-456, 676-687): the device RHS with the slab's
+    noise field equals the oracle's stencil given the same field"""
+    meta, A = O.load_case("ragged")
+    Pm, info = O.params_from_meta(meta)
+    Pm = Pm.copy()
+    Pm[O.PARAM_NAMES.index("u_noise_amp")] = 0.5
+    sim = P.Simulation(info["n1"], info["n2"], info["n3"], (info["L1"], info["L2"], info["L3"]), mode, Pm,
+                       initial=A["state"], init_solver=False, tile=FLAVOURS[flavour][0],
+                       recompute=FLAVOURS[flavour][1])
+    n = info["n1"] * info["n2"] * info["n3"]
+    noise = np.ctypeslib.as_array(P.lib().pft_model_noise(), shape=(n,)).copy()
+    assert np.abs(noise).max() > 0
+    t = meta["rhs_times"]["t1"]
+    dw, _ = P.rhs(sim, t)
+    K = dw.reshape((3,) + sim.N)[:, 2:-2, 2:-2, 2:-2]
+    sim.close()
+    g = O.make_grid(info)
+    w = O.pad(g, A["state"])
+    O.lib().pft_or_bcond(C.byref(g), O.ptr(Pm), t, O.ptr(w))
+    dwo = np.zeros_like(w)
+    O.lib().pft_or_stencil(C.byref(g), O.ptr(Pm), mode, O.ptr(w), O.ptr(noise), O.ptr(dwo))
+    assert np.array_equal(K, O.unpad(g, dwo))
