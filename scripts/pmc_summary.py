@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 runs of bench.py into profiles/pmc_summary.json.
 
-Inputs (directories written by scripts/gpu_profile.sh): a kernel-trace/--stats run and two PMC
+Inputs (directories written by scripts/evidence.sh): a kernel-trace/--stats run and two PMC
 runs (FETCH_SIZE, WRITE_SIZE -- separate passes, MI355X_MICROARCH.md "rocprofv3 PMC slots").
 Corrections (MI355X_MICROARCH.md "HBM"): FETCH_SIZE/WRITE_SIZE are in KiB; gfx950's FETCH_SIZE
 is only exact for calibrated access widths, so the ratio known/measured of the probe_copy_kernel
