@@ -44,8 +44,10 @@ HBM_PEAK_GBPS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # once + written once, perfect stencil reuse.  faithful: u, p, gl all evolved by the solver;
 # gl_static: dgl == 0 exploited (PFT_OPT_GL_STATIC)
 STAGE_DOUBLES_AUX = {False: {1: 9, 2: 12, 3: 15, 4: 18, 5: 18}, True: {1: 7, 2: 9, 3: 11, 4: 13, 5: 13}}
-# recompute path: stage s reads the arrays its input is built from, writes K_s (stage 5: x(t+h))
-STAGE_DOUBLES_RC = {False: {1: 6, 2: 9, 3: 12, 4: 12, 5: 15}, True: {1: 5, 2: 7, 3: 9, 4: 9, 5: 11}}
+# recompute path: stage s reads the arrays its input is built from, writes K_s (stage 5: x(t+h));
+# gl's K's are the literal zeros of dgl (PFT_GLK_LITERAL, never stored or loaded), so a stage
+# reads x of all 3 fields, the K's of u and p, and writes K_s of u and p (stage 5: all of x(t+h))
+STAGE_DOUBLES_RC = {False: {1: 5, 2: 7, 3: 9, 4: 9, 5: 12}, True: {1: 5, 2: 7, 3: 9, 4: 9, 5: 11}}
 SURVEY_BYTES_PER_CELL_STEP = 840   # unfused solver/RHS boundary accounting
 METRIC = "Mcells·RK-steps/s at 400³ grid, 1/2/4/8 MI355X; % HBM roofline"
 PUBLISHED_400_MODE1 = 351.88      # BASELINE.md 1, CC-HR-12nodes SigmaP1-P-smallsigma, 384 cores

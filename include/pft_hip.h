@@ -87,6 +87,10 @@ int pft_slab_set_recompute(pft_slab * s, int on);
 /* buffer written by stage 1..5 of the step on this slab's path (its boundary planes are what
    the z-neighbours need before the next stage) */
 int pft_slab_stage_output(const pft_slab * s, int stage);
+/* number of fields (u, p[, gl]) of that buffer the stage writes and the neighbours need; stage 6
+   = the speculative stage 1.  gl is left out under gl_static, and for K1..K4 on the recompute
+   path, where gl's K's are the literal zeros of dgl (equation.c:731) and never stored */
+int pft_slab_stage_fields(const pft_slab * s, int stage);
 
 /* host layout (reference padded, ghost thickness 2) <-> device layout, on the compute stream */
 int pft_slab_upload_host(pft_slab * s, int which, const double * host_padded);

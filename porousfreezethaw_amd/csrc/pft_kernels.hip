@@ -55,6 +55,12 @@
 #ifndef PFT_FUSED_WAVES
 #define PFT_FUSED_WAVES 3
 #endif
+// recompute path: the gl components of K1..K4 are the literal zeros of dgl (equation.c:731,874),
+// not arrays in HBM (42 instead of 54 doubles per cell-step, bit-identical).  An A/B build with
+// -DPFT_GLK_LITERAL=0 materialises them as the reference does.
+#ifndef PFT_GLK_LITERAL
+#define PFT_GLK_LITERAL 1
+#endif
 
 static __thread char g_err[256];
 
@@ -651,6 +657,16 @@ __device__ __forceinline__ void load_ops(const StageArgs& a, int q, long o, Ops&
 {
   r.x = ld2(a.x + q * a.fs + o);
   if (GLS && q == 2) return;                     // dgl == 0: the gl input is x (F4)
+#if PFT_GLK_LITERAL
+  if (q == 2) {
+    // gl's K's are the literal 0.0 the model's RHS writes for dgl (equation.c:731,874): never
+    // stored, never loaded; the stage combines still run on them (stage_in, stage 5), so the gl
+    // stage inputs and x(t+h) carry the reference's bits, signed zeros included
+    constexpr dbl2 z = {0.0, 0.0};
+    r.k1 = z; r.k2 = z; r.k3 = z; r.k4 = z;
+    return;
+  }
+#endif
   if (STAGE >= 2) r.k1 = ld2(a.k1 + q * a.fs + o);
   if (STAGE == 3) r.k2 = ld2(a.k2 + q * a.fs + o);
   if (STAGE >= 4) r.k3 = ld2(a.k3 + q * a.fs + o);
@@ -866,7 +882,7 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
     if (active) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
-        if (GLS && q == 2 && STAGE != 0) continue;
+        if (q == 2 && STAGE != 0 && (GLS || (PFT_GLK_LITERAL && STAGE <= 4))) continue;
         const dbl2 K = q == 0 ? dbl2{du[0], du[1]} : (q == 1 ? dbl2{dp[0], dp[1]} : dbl2{0.0, 0.0});
         const long e = q * a.fs + o;
         if (STAGE <= 4) {
@@ -1352,6 +1368,16 @@ int pft_slab_stage_output(const pft_slab* s, int stage)
   static const int rc_out[6] = {-1, PFT_BUF_K1, PFT_BUF_A0 /* K2 */, PFT_BUF_K3, PFT_BUF_K4, PFT_BUF_XN};
   if (stage < 1 || stage > 5) return -2;
   return slab_kind(s) == KFUSED ? rc_out[stage] : aux_out[stage];
+}
+
+int pft_slab_stage_fields(const pft_slab* s, int stage)
+{
+  // fields of a stage's output buffer that the stage writes (stage 6: the speculative stage 1):
+  // gl is not evolved under gl_static, and its K's are literal zeros on the recompute path
+  if (stage < 1 || stage > 6) return -2;
+  if (s->d.gl_static) return 2;
+  if (slab_kind(s) == KFUSED && PFT_GLK_LITERAL && stage != 5) return 2;
+  return 3;
 }
 
 static int run_stage(pft_slab* s, int stage, const double* in, double* kout, double* out, double t_stage,

@@ -200,10 +200,11 @@ static int run1(int stage, double ts, double coef, double h, int kb, int ke)
 	return stage == 6 ? pft_slab_stage_spec(R.slab, ts, kb, ke) : pft_slab_stage(R.slab, stage, ts, coef, h, kb, ke);
 }
 
-static int do_stage(int stage, double ts, double coef, double h, int nfields, long * launches)
+static int do_stage(int stage, double ts, double coef, double h, long * launches)
 {
 	pft_comm * c = comm();
 	const int out_buf = stage == 6 ? PFT_BUF_A1 : pft_slab_stage_output(R.slab, stage);
+	const int nfields = pft_slab_stage_fields(R.slab, stage);
 	const int tstage = stage == 6 ? 1 : stage;
 	int rc, n3;
 	if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 0);
@@ -239,7 +240,6 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	const double final_time = B->final_time, delta = B->delta, h_min = B->h_min;
 	int nonfinite, rc, ret = 0;
 	long attempted = 0, launches = 0;
-	const int nf = R.opt_gls ? 2 : 3;     /* fields whose stage values change */
 	int spec, k1_valid = 0;               /* K1 holds f(t, x) for the current t and x */
 
 	if((rc = ensure_slab())) return rc;
@@ -267,16 +267,16 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 		/* the error norm accumulator is reset by its publication on the speculative path */
 		if((!spec || attempted == 0) && (rc = pft_slab_eps_reset(R.slab))) return rc;
 		/* K1 = f(t,x); aux = x + K1 h/3 ... K5 = f(t+h, aux); error norm; x(t+h) candidate */
-		if(!(spec && k1_valid) && (rc = do_stage(1, t, h3, h, nf, &launches))) return rc;  /* :373-389 */
+		if(!(spec && k1_valid) && (rc = do_stage(1, t, h3, h, &launches))) return rc;  /* :373-389 */
 		k1_valid = 1;
-		if((rc = do_stage(2, t+h3, h6, h, nf, &launches))) return rc;    /* :392-409 */
-		if((rc = do_stage(3, t+h3, h8, h, nf, &launches))) return rc;    /* :412-429 */
-		if((rc = do_stage(4, t+h2, h,  h, nf, &launches))) return rc;    /* :432-450 */
-		if((rc = do_stage(5, t+h,  h3, h, nf, &launches))) return rc;    /* :453,507-524,657-668 */
+		if((rc = do_stage(2, t+h3, h6, h, &launches))) return rc;    /* :392-409 */
+		if((rc = do_stage(3, t+h3, h8, h, &launches))) return rc;    /* :412-429 */
+		if((rc = do_stage(4, t+h2, h,  h, &launches))) return rc;    /* :432-450 */
+		if((rc = do_stage(5, t+h,  h3, h, &launches))) return rc;    /* :453,507-524,657-668 */
 		if((rc = pft_comm_allreduce_eps(c))) return rc;                          /* :572 */
 		if(spec) {
 			if((rc = pft_slab_eps_mark(R.slab))) return rc;
-			if((rc = do_stage(6, t+h, 0.0, h, nf, &launches))) return rc;
+			if((rc = do_stage(6, t+h, 0.0, h, &launches))) return rc;
 		}
 		if((rc = pft_slab_eps_fetch(R.slab, &eps, &nonfinite))) return rc;
 		if(R.opt_timing) pft_slab_timing_collect(R.slab, R.stats.stage_ms, R.stats.stage_n);
