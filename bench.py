@@ -46,8 +46,9 @@ HBM_PEAK_GBPS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 STAGE_DOUBLES_AUX = {False: {1: 9, 2: 12, 3: 15, 4: 18, 5: 18}, True: {1: 7, 2: 9, 3: 11, 4: 13, 5: 13}}
 # recompute path: stage s reads the arrays its input is built from, writes K_s (stage 5: x(t+h));
 # gl's K's are the literal zeros of dgl (PFT_GLK_LITERAL, never stored or loaded), so a stage
-# reads x of all 3 fields, the K's of u and p, and writes K_s of u and p (stage 5: all of x(t+h))
-STAGE_DOUBLES_RC = {False: {1: 5, 2: 7, 3: 9, 4: 9, 5: 12}, True: {1: 5, 2: 7, 3: 9, 4: 9, 5: 11}}
+# reads x of all 3 fields, the K's of u and p, and writes K_s of u and p (stage 5: all of x(t+h));
+# stage 2 stores S = K1 + K2, so stage 3 reads x and S (PFT_K12_SUM)
+STAGE_DOUBLES_RC = {False: {1: 5, 2: 7, 3: 7, 4: 9, 5: 12}, True: {1: 5, 2: 7, 3: 7, 4: 9, 5: 11}}
 SURVEY_BYTES_PER_CELL_STEP = 840   # unfused solver/RHS boundary accounting
 METRIC = "Mcells·RK-steps/s at 400³ grid, 1/2/4/8 MI355X; % HBM roofline"
 PUBLISHED_400_MODE1 = 351.88      # BASELINE.md 1, CC-HR-12nodes SigmaP1-P-smallsigma, 384 cores
@@ -275,7 +276,7 @@ def kernel_name(stage, a, rc_path, n1):
         return f"merson_stage<{stage}, {a.mode}, {gls}>"
     wx = (16 if stage <= 2 else 32) if a.tile == 1 else a.tile
     if rc_path:
-        return f"merson_fused<{stage}, {a.mode}, {gls}, {wx}>"
+        return f"merson_fused<{stage}, {a.mode}, {gls}>"
     return f"merson_tile<{stage}, {a.mode}, {gls}, {wx}>"
 
 

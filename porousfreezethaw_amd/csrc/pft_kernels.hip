@@ -31,6 +31,12 @@
 #define PFT_BLOCK 256
 #define PFT_TRING 8
 
+// recompute path: the gl components of K1..K4 are the literal zeros of dgl (equation.c:731,874),
+// not arrays in HBM (42 instead of 54 doubles per cell-step, bit-identical).  An A/B build with
+// -DPFT_GLK_LITERAL=0 materialises them as the reference does.
+#ifndef PFT_GLK_LITERAL
+#define PFT_GLK_LITERAL 1
+#endif
 // stage 5 of the recompute kernel keeps the combine operands of planes k and k+1 in registers
 // (measured 0.52 vs 0.65 ms at 400^3: re-loading them one plane later misses the 4 MiB L2)
 #ifndef PFT_S5_RELOAD
@@ -47,19 +53,33 @@
 #define PFT_S5_GLZERO 1
 #endif
 #ifndef PFT_S5_FACE
-#define PFT_S5_FACE 0
+#define PFT_S5_FACE PFT_GLK_LITERAL
 #endif
+// stages with the two-deep z pipeline.  Measured at 400^3 (A/B, same box): faithful stages 3-4
+// 0.258 vs 0.288 / 0.296 ms once gl's K's became literals (operands as few as gl_static's); stage 1
+// no gain (its one input is x); stage 2 0.214-0.221 vs 0.228-0.230 before it carried K1 for the
+// K1 + K2 sum (PFT_K12_SUM), 0.250 vs 0.238 after (180 VGPRs: 2 waves)
 #ifndef PFT_DEEP_MASK
-#define PFT_DEEP_MASK ((1 << 3) | (1 << 4))   // stages with the two-deep z pipeline
+#define PFT_DEEP_MASK ((1 << 3) | (1 << 4))
+#endif
+#ifndef PFT_DEEP_ALL
+#define PFT_DEEP_ALL PFT_GLK_LITERAL
 #endif
 #ifndef PFT_FUSED_WAVES
 #define PFT_FUSED_WAVES 3
 #endif
-// recompute path: the gl components of K1..K4 are the literal zeros of dgl (equation.c:731,874),
-// not arrays in HBM (42 instead of 54 doubles per cell-step, bit-identical).  An A/B build with
-// -DPFT_GLK_LITERAL=0 materialises them as the reference does.
-#ifndef PFT_GLK_LITERAL
-#define PFT_GLK_LITERAL 1
+#ifndef PFT_KUNROLL
+#define PFT_KUNROLL 1
+#endif
+// recompute path: stage 2 stores S = K1 + K2 (the sum stage 3's input combine forms,
+// hybrid2.c:408, same operands) in place of K2, so stage 3 reads x and S instead of x, K1, K2
+#ifndef PFT_K12_SUM
+#define PFT_K12_SUM 1
+#endif
+// stage 2 re-loads K1 of plane k for the sum (loaded one plane earlier: an L2 hit) instead of
+// keeping it in registers
+#ifndef PFT_K12_RELOAD
+#define PFT_K12_RELOAD 0
 #endif
 
 static __thread char g_err[256];
@@ -181,6 +201,14 @@ __device__ __forceinline__ void rhs_cell_f(const pft_consts& c, const Col& u, co
 {
   constexpr bool FLUX = MODE != 10 && MODE != 11;
   const double pc = p.c, gc = g.c, uc = u.c;
+#ifdef PFT_ABLATE_RHS
+  // diagnostic build only (never shipped): same loads and stores, trivial arithmetic
+  fxp = FaceT{u.xp, p.xp};
+  fzp = FaceT{u.zp, p.zp};
+  du = ((fxm.prod + u.ym) + (u.yp + fzm.prod)) + (un + gc);
+  dp = ((fxm.dp + p.ym) + (p.yp + fzm.dp)) + (pc + g.xp + g.ym + g.yp + g.zp);
+  return;
+#endif
   const double rho = gc * c.rho_g + (1.0 - gc) * (pc * c.rho_i + (1.0 - pc) * c.rho_w);
   const double cp = gc * c.cp_g + (1.0 - gc) * (pc * c.cp_i + (1.0 - pc) * c.cp_w);
   const double wi = fmax(0.0, 1.0 - c.zeta * gc);
@@ -246,6 +274,7 @@ struct StageArgs {
   // recompute path (merson_fused): the stage input is rebuilt from x and the K's
   const double* k2;    // K2 (stored only on this path; the reference aliases it with K3)
   double cin;          // coefficient of the stage-input combine: h3, h6, h8, h for stages 2..5
+  int gwx, gty;        // merson_fused tile: gwx cell pairs x gty rows (fused_geometry)
 };
 
 __device__ __forceinline__ int xcd_remap(int b, int n)
@@ -450,6 +479,9 @@ __global__ __launch_bounds__(PFT_BLOCK) void merson_stage(StageArgs a, pft_const
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
+// LDS doubles per field and plane of merson_fused: (2 gwx + 4)(gty + 2) <= 680 (64 x 8 tiles)
+#define PFT_FUSED_LF 680
+
 template <int WX>
 struct TileGeo {
   static constexpr int TX = 2 * WX;              // cells in x
@@ -460,8 +492,28 @@ struct TileGeo {
   static constexpr int NH = LW + 2 * TY;         // halo pairs per field: 2 rows of LW/2, 2 per inner row
 };
 
-__device__ __forceinline__ dbl2 ld2(const double* p) { return *reinterpret_cast<const dbl2*>(p); }
-__device__ __forceinline__ void st2(double* p, dbl2 v) { *reinterpret_cast<dbl2*>(p) = v; }
+#ifndef PFT_NT_STORE
+#define PFT_NT_STORE 0
+#endif
+#ifndef PFT_NT_LOAD
+#define PFT_NT_LOAD 0
+#endif
+__device__ __forceinline__ dbl2 ld2(const double* p)
+{
+#if PFT_NT_LOAD
+  return __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(p));
+#else
+  return *reinterpret_cast<const dbl2*>(p);
+#endif
+}
+__device__ __forceinline__ void st2(double* p, dbl2 v)
+{
+#if PFT_NT_STORE
+  __builtin_nontemporal_store(v, reinterpret_cast<dbl2*>(p));
+#else
+  *reinterpret_cast<dbl2*>(p) = v;
+#endif
+}
 // store a pair with its halves exchanged when sw = 1 (two 8-byte stores at per-thread offsets)
 __device__ __forceinline__ void st2x(double* p, dbl2 v, int sw)
 {
@@ -667,8 +719,8 @@ __device__ __forceinline__ void load_ops(const StageArgs& a, int q, long o, Ops&
     return;
   }
 #endif
-  if (STAGE >= 2) r.k1 = ld2(a.k1 + q * a.fs + o);
-  if (STAGE == 3) r.k2 = ld2(a.k2 + q * a.fs + o);
+  if (STAGE >= 2 && !(STAGE == 3 && PFT_K12_SUM)) r.k1 = ld2(a.k1 + q * a.fs + o);
+  if (STAGE == 3) r.k2 = ld2(a.k2 + q * a.fs + o);   // K2, or S = K1 + K2 (PFT_K12_SUM)
   if (STAGE >= 4) r.k3 = ld2(a.k3 + q * a.fs + o);
   if (STAGE == 5) r.k4 = ld2(a.k4 + q * a.fs + o);
 }
@@ -681,7 +733,7 @@ __device__ __forceinline__ dbl2 stage_in(const StageArgs& a, int q, const Ops& r
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     if (STAGE == 2) v[s] = r.k1[s] * a.cin + r.x[s];                                      // hybrid2.c:388
-    if (STAGE == 3) v[s] = (r.k1[s] + r.k2[s]) * a.cin + r.x[s];                          // :408
+    if (STAGE == 3) v[s] = (PFT_K12_SUM ? r.k2[s] : r.k1[s] + r.k2[s]) * a.cin + r.x[s];  // :408
     if (STAGE == 4) v[s] = (r.k1[s] + 3.0 * r.k3[s]) * a.cin + r.x[s];                    // :428
     if (STAGE == 5) v[s] = (0.5 * r.k1[s] - 1.5 * r.k3[s] + 2.0 * r.k4[s]) * a.cin + r.x[s];  // :449
   }
@@ -699,31 +751,36 @@ __device__ __forceinline__ void keep5(int q, const Ops& r, dbl2& x, dbl2& k1, db
   for (int s = 0; s < 2; ++s) E[s] = 0.2 * r.k1[s] - 0.9 * r.k3[s] + 0.8 * r.k4[s];   // hybrid2.c:521 prefix
 }
 
-template <int STAGE, int MODE, bool GLS, int WX>
-__global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_S5_WAVES2 && STAGE == 5) || (GLS && ((PFT_DEEP_MASK >> STAGE) & 1)) ? 2 : PFT_FUSED_WAVES))) void merson_fused(StageArgs a, pft_consts c)
+template <int STAGE, int MODE, bool GLS>
+__global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_S5_WAVES2 && STAGE == 5) || ((GLS || PFT_DEEP_ALL) && ((PFT_DEEP_MASK >> STAGE) & 1)) ? 2 : PFT_FUSED_WAVES))) void merson_fused(StageArgs a, pft_consts c)
 {
-  using G = TileGeo<WX>;
-  __shared__ __attribute__((aligned(16))) double lds[2][3][G::LF];
+  // tile geometry chosen by the host per grid (fused_geometry): gwx pairs x gty rows, so that the
+  // tiles fit n1 and n2 without mostly-idle edge workgroups (n1 = 200: 50 x 10 cells)
+  const int WX = a.gwx, TY = a.gty, TX = 2 * WX, LW = TX + 4, LH = TY + 2, NH = LW + 2 * TY;
+  __shared__ __attribute__((aligned(16))) double lds[2][3][PFT_FUSED_LF];
 
-  const int ntx = (a.n1 + G::TX - 1) / G::TX;
+  const int ntx = (a.n1 + TX - 1) / TX;
   const int lin = xcd_remap(blockIdx.x, a.ntile * a.nchunk);
   const int tile = lin % a.ntile, chunk = lin / a.ntile;
-  const int x0 = (tile % ntx) * G::TX, y0 = (tile / ntx) * G::TY;
-  const int tx = threadIdx.x % WX, ty = threadIdx.x / WX;
+  const int x0 = (tile % ntx) * TX, y0 = (tile / ntx) * TY;
+  // threads beyond the WX x TY tile (256 > WX * TY) shadow the tile's last thread: the same loads
+  // and LDS writes (same values to the same slots), no global stores
+  const int tt = min((int)threadIdx.x, WX * TY - 1);
+  const int tx = tt % WX, ty = tt / WX;
   const int i0 = x0 + 2 * tx, j = y0 + ty;
-  const bool active = (i0 < a.n1) && (j < a.n2);
+  const bool active = (i0 < a.n1) && (j < a.n2) && (int)threadIdx.x < WX * TY;
   const long po = (long)(j < a.n2 ? j : a.n2 - 1) * a.n1 + (i0 < a.n1 ? i0 : a.n1 - 2);
   const int kb = a.k_begin + chunk * a.kz;
   const int ke = min(kb + a.kz, a.k_end);
-  const int lo = (ty + 1) * G::LW + 2 + 2 * tx;
+  const int lo = (ty + 1) * LW + 2 + 2 * tx;
 
   const int t = threadIdx.x;
-  const bool hact = t < 3 * G::NH;
-  const int hf = hact ? t / G::NH : 0, h = hact ? t % G::NH : 0;
+  const bool hact = t < 3 * NH;
+  const int hf = hact ? t / NH : 0, h = hact ? t % NH : 0;
   int hr, hcp;
-  if (h < G::LW / 2) { hr = 0; hcp = h; }
-  else if (h < G::LW) { hr = G::LH - 1; hcp = h - G::LW / 2; }
-  else { const int q = h - G::LW; hr = 1 + q / 2; hcp = (q & 1) ? G::LW / 2 - 1 : 0; }
+  if (h < LW / 2) { hr = 0; hcp = h; }
+  else if (h < LW) { hr = LH - 1; hcp = h - LW / 2; }
+  else { const int q = h - LW; hr = 1 + q / 2; hcp = (q & 1) ? LW / 2 - 1 : 0; }
   const int hi = x0 - 2 + 2 * hcp, hj = y0 + hr - 1;
   // Walls in LDS: a halo pair outside the domain holds the mirror image the reference's ghost
   // fill puts there (equation.c:137-174: ghost -1-m = interior m), so the stencil reads its x/y
@@ -732,7 +789,7 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
   const bool hswap = hi < 0 || hi >= a.n1;
   const long hp = (long)(hj < 0 ? 0 : (hj >= a.n2 ? a.n2 - 1 : hj)) * a.n1 +
                   (hi < 0 ? 0 : (hi >= a.n1 ? a.n1 - 2 : hi));
-  const int hl = hr * G::LW + 2 * hcp;
+  const int hl = hr * LW + 2 * hcp;
   // an inactive pair just right of the domain (partial tile) is the mirror of the last pair.
   // Swapped pairs are stored as two 8-byte halves at exchanged offsets (per-thread constants),
   // not through per-store selects.
@@ -752,9 +809,12 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
   // one-deep pipeline waits for its loads before the stencil).  It costs the operand registers:
   // 198 VGPRs = 2 waves/SIMD for stages 3-4.  Measured at 400^3: gl_static stages 3-4 0.275 vs
   // 0.294 ms; faithful (3 evolving fields, more operands) 0.376 vs 0.370 -- kept off there.
-  constexpr bool DEEP = GLS && ((PFT_DEEP_MASK >> STAGE) & 1) != 0 && STAGE >= 1 && STAGE <= 4;
+  constexpr bool DEEP = (GLS || PFT_DEEP_ALL) && ((PFT_DEEP_MASK >> STAGE) & 1) != 0 && STAGE >= 1 && STAGE <= 4;
   Ops pn[3], ph;                       // DEEP: operands of plane k+1 (centre, halo pair)
   FaceT fz[2];                         // z-face below plane k of each cell of the pair
+  constexpr bool SUM2 = STAGE == 2 && PFT_K12_SUM;
+  constexpr bool SUM2K = SUM2 && !PFT_K12_RELOAD;   // K1 carried in registers
+  dbl2 s2c[3], s2n[3];                 // SUM2: K1 of planes k and k+1 (the stored sum's operand)
 #ifdef PFT_S5_KEEP
   // stage 5 keeps x, K1, K4 and the K1/K3/K4 part of the error norm of planes k and k+1
   dbl2 cx[3], ck1[3], ck4[3], cE[3], nx[3], nk1[3], nk4[3], nE[3];
@@ -767,6 +827,7 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
       Ops cop;
       load_ops<STAGE, GLS>(a, q, o0, cop);
       zc[q] = stage_in<STAGE, GLS>(a, q, cop);
+      if constexpr (SUM2K) s2c[q] = cop.k1;
 #ifdef PFT_S5_KEEP
       if (STAGE == 5) keep5<GLS>(q, cop, cx[q], ck1[q], ck4[q], cE[q]);
 #endif
@@ -800,6 +861,7 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
     }
     __syncthreads();
   }
+#pragma unroll PFT_KUNROLL
   for (int k = kb; k < ke; ++k) {
     const long o = (long)(k + 1) * a.plane + po;
     const bool top = (k == a.n3 - 1) && !a.has_above;
@@ -810,10 +872,12 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
       for (int q = 0; q < 3; ++q) {
         if constexpr (DEEP) {
           zp[q] = stage_in<STAGE, GLS>(a, q, pn[q]);
+          if constexpr (SUM2K) s2n[q] = pn[q].k1;
         } else {
           Ops nop;
           load_ops<STAGE, GLS>(a, q, o + a.plane, nop);
           zp[q] = stage_in<STAGE, GLS>(a, q, nop);
+          if constexpr (SUM2K) s2n[q] = nop.k1;
 #ifdef PFT_S5_KEEP
           if (STAGE == 5) keep5<GLS>(q, nop, nx[q], nk1[q], nk4[q], nE[q]);
 #endif
@@ -862,8 +926,8 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
         // x/y neighbours straight from LDS: the walls' mirror values are in the halo
         col[q].xm = s == 0 ? L[lo - 1] : zc[q][0];
         col[q].xp = s == 0 ? zc[q][1] : L[lo + 2];
-        col[q].ym = L[lo - G::LW + s];
-        col[q].yp = L[lo + G::LW + s];
+        col[q].ym = L[lo - LW + s];
+        col[q].yp = L[lo + LW + s];
         col[q].zm = zm[q][s];
         col[q].zp = zp[q][s];
       }
@@ -885,7 +949,13 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
         if (q == 2 && STAGE != 0 && (GLS || (PFT_GLK_LITERAL && STAGE <= 4))) continue;
         const dbl2 K = q == 0 ? dbl2{du[0], du[1]} : (q == 1 ? dbl2{dp[0], dp[1]} : dbl2{0.0, 0.0});
         const long e = q * a.fs + o;
-        if (STAGE <= 4) {
+        if (SUM2) {
+          dbl2 S;
+          const dbl2 k1c = SUM2K ? s2c[q] : ((PFT_GLK_LITERAL && q == 2) ? dbl2{0.0, 0.0} : ld2(a.k1 + e));
+#pragma unroll
+          for (int s = 0; s < 2; ++s) S[s] = k1c[s] + K[s];   // K1 + K2, hybrid2.c:408
+          st2(a.kout + e, S);
+        } else if (STAGE <= 4) {
           st2(a.kout + e, K);
         } else {
           // operands of plane k again (loaded one iteration ago: an L2 hit; keeping them in
@@ -928,6 +998,7 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
     for (int q = 0; q < 3; ++q) {
       zm[q] = zc[q];
       zc[q] = zp[q];
+      if constexpr (SUM2K) s2c[q] = s2n[q];
 #ifdef PFT_S5_KEEP
       if (STAGE == 5) { cx[q] = nx[q]; ck1[q] = nk1[q]; ck4[q] = nk4[q]; cE[q] = nE[q]; }
 #endif
@@ -1267,10 +1338,9 @@ template <int STAGE, int MODE, bool GLS>
 static int kernel_occupancy(int kind, int wx)
 {
   static int cache[3][2] = {{0, 0}, {0, 0}, {0, 0}};
-  int& n = cache[kind][wx == 16 ? 1 : 0];
+  int& n = cache[kind][(kind != KFUSED && wx == 16) ? 1 : 0];
   if (n) return n;
-  const void* f = kind == KFUSED ? (wx == 16 ? (const void*)merson_fused<STAGE, MODE, GLS, 16>
-                                             : (const void*)merson_fused<STAGE, MODE, GLS, 32>)
+  const void* f = kind == KFUSED ? (const void*)merson_fused<STAGE, MODE, GLS>
                 : kind == KTILE ? (wx == 16 ? (const void*)merson_tile<STAGE, MODE, GLS, 16>
                                             : (const void*)merson_tile<STAGE, MODE, GLS, 32>)
                                 : (const void*)merson_stage<STAGE, MODE, GLS>;
@@ -1308,10 +1378,7 @@ template <int STAGE, int MODE, bool GLS>
 static void launch_kernel(int kind, int wx, dim3 g, hipStream_t st, const StageArgs& a, const pft_consts& c)
 {
   if (kind == KFUSED) {
-    if (wx == 16)
-      merson_fused<STAGE, MODE, GLS, 16><<<g, PFT_BLOCK, 0, st>>>(a, c);
-    else
-      merson_fused<STAGE, MODE, GLS, 32><<<g, PFT_BLOCK, 0, st>>>(a, c);
+    merson_fused<STAGE, MODE, GLS><<<g, PFT_BLOCK, 0, st>>>(a, c);
   } else if (kind == KTILE) {
     if (wx == 16)
       merson_tile<STAGE, MODE, GLS, 16><<<g, PFT_BLOCK, 0, st>>>(a, c);
@@ -1380,6 +1447,42 @@ int pft_slab_stage_fields(const pft_slab* s, int stage)
   return 3;
 }
 
+// merson_fused tile: wx cell pairs x ty rows, 256 threads.  Limits: wx * ty <= 256 threads, the
+// halo ring (2 wx + 4 + 2 ty pairs per field, 3 fields) loaded by one pass of the 256 threads,
+// (2 wx + 4)(ty + 2) <= PFT_FUSED_LF doubles of LDS per field and plane.
+static bool fused_geometry_ok(int wx, int ty)
+{
+  return wx >= 4 && ty >= 1 && wx * ty <= PFT_BLOCK && 3 * (2 * wx + 4 + 2 * ty) <= PFT_BLOCK &&
+         (2 * wx + 4) * (ty + 2) <= PFT_FUSED_LF;
+}
+
+// automatic choice: 16..40 pairs wide (rows of 256-640 B), the tallest rows count that fits, and
+// of those the tile whose workgroups carry the fewest idle lanes over the whole plane (edge tiles,
+// threads beyond wx * ty); within 0.5% the wider.  Measured: with 64 x 8 tiles at n1 = 200 a
+// quarter of the workgroups are 7/8 idle; a z-march of 64-wide tiles streams at 4.7-4.9 TB/s
+// there and at 5.2-5.4 TB/s when n1 is a multiple of 64 (scripts/probes/stream_probe.hip).
+// n1 = 200 and 400: 25 x 10 pairs (50 x 10 cells), all lanes but 6 busy.
+static void fused_geometry(int n1, int n2, int* wx_out, int* ty_out)
+{
+  const int np = n1 / 2;
+  double best = -1.0;
+  int bw = 32, bt = 8;
+  for (int wx = 16; wx <= 40; ++wx) {
+    int ty = PFT_BLOCK / wx;
+    while (ty > 1 && !fused_geometry_ok(wx, ty)) --ty;
+    if (!fused_geometry_ok(wx, ty)) continue;
+    const long lanes = (long)((np + wx - 1) / wx) * ((n2 + ty - 1) / ty) * PFT_BLOCK;
+    const double eff = (double)np * n2 / (double)lanes;
+    if (eff >= best - 0.005) {
+      if (eff > best) best = eff;
+      bw = wx;
+      bt = ty;
+    }
+  }
+  *wx_out = bw;
+  *ty_out = bt;
+}
+
 static int run_stage(pft_slab* s, int stage, const double* in, double* kout, double* out, double t_stage,
                      double coef, double h, int k_begin, int k_end, int gls, int kind)
 {
@@ -1413,7 +1516,16 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   // tile width: 1 = per stage (measured at 400^3: the VALU-bound stages 0-2 run faster on 32x16
   // tiles -- fewer idle lanes at the x edge, 200 = 6.25 x 32 -- the HBM-bound stages 3-5 on 64x8)
   const int wx = kind == KCACHE ? 0 : s->tile_wx == 1 ? (stage <= 2 ? 16 : 32) : s->tile_wx;
-  if (wx) {
+  if (kind == KFUSED) {
+    if (s->tile_wx == 1) {
+      fused_geometry(s->d.n1, s->d.n2, &a.gwx, &a.gty);
+    } else {
+      a.gwx = s->tile_wx;
+      a.gty = PFT_BLOCK / s->tile_wx;
+    }
+    if (!fused_geometry_ok(a.gwx, a.gty)) return -2;
+    a.ntile = ((s->d.n1 + 2 * a.gwx - 1) / (2 * a.gwx)) * ((s->d.n2 + a.gty - 1) / a.gty);
+  } else if (wx) {
     const int TX = 2 * wx, TY = PFT_BLOCK / wx;
     a.ntile = ((s->d.n1 + TX - 1) / TX) * ((s->d.n2 + TY - 1) / TY);
   } else {
