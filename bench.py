@@ -64,6 +64,9 @@ def parse():
                     help="N>1 weak-scaling family (module docstring)")
     ap.add_argument("--literal-cube", action="store_true",
                     help="L1 = L2 = L3 = 0.06 m: G x G x G cells (SURVEY 8(d) secondary number)")
+    ap.add_argument("--domain", default=None,
+                    help="L1,L2,L3 in m (diagnostics): n_d = L_d * grid_nodes / max L, e.g. 0.06,0.06,0.015 "
+                         "with --grid-nodes 400 is one rank's 400x400x100 slab of the 800^3 8-way case")
     ap.add_argument("--mode", type=int, default=0, help="calc_mode (0 GradP, 1 SigmaP1-P, 2 Temp)")
     ap.add_argument("--gl-static", action="store_true", help="exploit dgl == 0 (bit-identical)")
     ap.add_argument("--kz", type=int, default=0, help="planes per workgroup z-march (default 0 = automatic)")
@@ -128,7 +131,7 @@ def main():
         L.pft_hip_device_sync()
 
     # ---- workload -------------------------------------------------------------------------
-    gn, base, (n1, n2, total_n3), Ls = workload(a.grid_nodes, world, a.shape, a.literal_cube, a.mode)
+    gn, base, (n1, n2, total_n3), Ls = workload(a.grid_nodes, world, a.shape, a.literal_cube, a.mode, a.domain)
     prm = P.params_array(base)
     beads = np.load(os.path.join(REPO, "tests", "golden", "beads.npy"))
     t0 = time.time()
@@ -257,9 +260,11 @@ def main():
         dist.destroy_process_group()
 
 
-def workload(grid_nodes, world, shape="cube", literal_cube=False, mode=0):
+def workload(grid_nodes, world, shape="cube", literal_cube=False, mode=0, domain=None):
     """(G, Params dict, (n1, n2, total_n3), (L1, L2, L3)) of the N = world benchmark case"""
     Lc = (PR.float_val("0.06"),) * 3 if literal_cube else None
+    if domain:
+        Lc = tuple(PR.float_val(v) for v in domain.split(","))
     if shape == "cube" and world > 1:
         gn = int(round(grid_nodes * world ** (1.0 / 3.0) / 4.0)) * 4
         base = PR.default_params(grid_nodes=gn, calc_mode=mode, L=Lc)

@@ -1535,22 +1535,24 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   if (s->kz > 0) {
     a.kz = s->kz;
   } else {
-    // automatic: the whole launch resident in one round (a second, partial round of workgroups
-    // costs more than a longer z-march, and every chunk boundary re-reads two planes of all
-    // operands).  VALU-bound stages 1-2 take the most chunks that fit (every resident wave
-    // helps); HBM-bound stages 3-5 take the chunk count that spreads the workgroups most evenly
-    // over the CUs (measured at 400^3, 100 tiles: 500 workgroups = 2 per CU beat 700 = 2-3 per CU).
+    // automatic: a CU runs `occ` workgroups at a time, so a chunk count costs
+    //   rounds x (kz + 2) = ceil(ceil(workgroups / CUs) / occ) x (planes per chunk + the two
+    // planes a chunk re-reads below and above); the cheapest count wins (more chunks only when 5% cheaper).
+    // Measured on a 400 x 400 x 100 slab (320 tiles; one 800^3 8-way rank), stages 4-5 at 2
+    // workgroups per CU: 3 chunks (960 workgroups, 2 rounds) 0.261 / 0.349 ms against 0.314 /
+    // 0.436 for the one-round choice (1 chunk: 64 CUs with 2 workgroups, 192 with 1); at 400^3
+    // (80 tiles) it keeps the one-round choices (stage 5: 6 chunks, 480 workgroups).
     const int occ = stage_occupancy(stage, mode, gls, kind, wx);
-    const int max_nch = std::max(1, std::min(nplanes, s->n_cu * occ / a.ntile));
-    int best_nch = max_nch;
-    if (stage >= 3) {
-      double best_even = -1.0;
-      for (int nch = 1; nch <= max_nch; ++nch) {
-        const long nb = (long)a.ntile * nch;
-        const long m = (nb + s->n_cu - 1) / s->n_cu;            // workgroups on the busiest CU
-        const double even = (double)nb / (double)(m * s->n_cu);
-        if (even >= best_even) { best_even = even; best_nch = nch; }
-      }
+    int best_nch = 1;
+    long best_cost = -1;
+    for (int nch = 1; nch <= nplanes; ++nch) {
+      const int kz = (nplanes + nch - 1) / nch;
+      if (nch > 1 && kz == (nplanes + nch - 2) / (nch - 1)) continue;   // same kz as nch - 1
+      const long nb = (long)a.ntile * ((nplanes + kz - 1) / kz);
+      const long per_cu = (nb + s->n_cu - 1) / s->n_cu;
+      const long rounds = (per_cu + occ - 1) / occ;
+      const long cost = rounds * (kz + 2);
+      if (best_cost < 0 || 20 * cost < 19 * best_cost) { best_cost = cost; best_nch = nch; }
     }
     a.kz = (nplanes + best_nch - 1) / best_nch;
   }
