@@ -81,6 +81,10 @@ def parse():
     ap.add_argument("--host-boundary", action="store_true",
                     help="timed call is one RK_MPI_SA_solve-style call: x copied host->device at entry "
                          "and back at exit (PCIe-inclusive rate; never the headline value)")
+    ap.add_argument("--self-exchange", action="store_true",
+                    help="diagnostic, 1 GPU: run the N>1 stage pipeline (boundary planes first, RCCL halo "
+                         "exchange on the comm stream beside the interior sweep, RCCL eps max) with a "
+                         "1-rank communicator exchanging with itself; never the headline value")
     ap.add_argument("--probe", type=int, default=0,
                     help="after the run, launch the 8-B/lane copy probe this many times "
                          "(rocprofv3 FETCH_SIZE/WRITE_SIZE calibration, known bytes)")
@@ -89,6 +93,10 @@ def parse():
 
 def main():
     a = parse()
+    # stdout carries exactly one JSON line: anything else written to fd 1 (RCCL's version banner
+    # at communicator init, library diagnostics) goes to stderr
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     rc_path = (not a.no_recompute) and a.tile != 0
     STAGE_DOUBLES = STAGE_DOUBLES_RC if rc_path else STAGE_DOUBLES_AUX
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -123,6 +131,15 @@ def main():
         L.pft_comm_set_current(comm)
     else:
         L.pft_hip_set_device(dev)
+        if a.self_exchange:
+            uid = (C.c_char * 128)()
+            assert L.pft_comm_get_unique_id(uid) == 0
+            comm = C.c_void_p()
+            rc = L.pft_comm_init_rccl(C.byref(comm), 1, 0, uid, dev)
+            if rc:
+                sys.exit(f"pft_comm_init_rccl failed ({rc})")
+            assert L.pft_comm_set_self_exchange(comm, 1) == 0
+            L.pft_comm_set_current(comm)
     L.pft_solver_set_option(P.PFT_OPT_DEVICE, dev)
 
     def barrier():
@@ -224,7 +241,7 @@ def main():
                    "calc_mode": a.mode, "cells": cells_total, "parallelism": f"zslab{world}",
                    "gl_static": a.gl_static, "kz": a.kz or "auto", "tile": a.tile, "recompute": not a.no_recompute,
                    "accepted_steps_total": int(sim.system.steps), "t_end": sim.t,
-                   "host_boundary": a.host_boundary},
+                   "host_boundary": a.host_boundary, "self_exchange": a.self_exchange},
         "roofline": roof,
         "fused_effective_GBps": round(step_bytes * cells_total * steps / el / 1e9 / world, 1),
         "survey_840B_equiv_GBps": round(SURVEY_BYTES_PER_CELL_STEP * cells_total * steps / el / 1e9 / world, 1),
@@ -255,7 +272,8 @@ def main():
         L.pft_comm_set_current(None)
         L.pft_comm_destroy(comm)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist is not None:
         dist.destroy_process_group()
 

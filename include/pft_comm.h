@@ -38,6 +38,14 @@ int pft_comm_loopback_rank(pft_comm * group, int rank, pft_comm ** mine);
 int pft_comm_destroy(pft_comm * c);
 
 int pft_comm_rank(const pft_comm * c);
+/* 1 when the stage pipeline splits boundary planes from the interior and exchanges halos
+   (more than one rank, or the self-exchange diagnostic) */
+int pft_comm_splits(const pft_comm * c);
+/* diagnostic, 1-rank RCCL communicator only: run the multi-rank stage pipeline on one GPU, the
+   halo exchange sending the slab's boundary planes to its own ghost planes (never read by a
+   single slab) and the eps max through ncclAllReduce -- the per-rank cost of the N > 1 path
+   without the xGMI transfer time (bench.py --self-exchange) */
+int pft_comm_set_self_exchange(pft_comm * c, int on);
 int pft_comm_size(const pft_comm * c);
 const char * pft_comm_kind(const pft_comm * c);
 

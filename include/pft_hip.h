@@ -103,6 +103,8 @@ int pft_slab_download_host(pft_slab * s, int which, double * host_padded);
    range (for boundary-first splitting), -1/-1 = all planes. */
 int pft_slab_stage(pft_slab * s, int stage, double t_stage, double coef, double h,
                    int k_begin, int k_end);
+/* k_begin value selecting the slab's two boundary planes (0 and n3-1) in one launch */
+#define PFT_K_BOUNDARY (-2)
 
 /* K = f(input) only (RK_RightHandSide semantics), input/output buffer indices */
 int pft_slab_rhs(pft_slab * s, int in_buf, int out_buf, double t);

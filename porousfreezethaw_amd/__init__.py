@@ -129,6 +129,8 @@ def lib():
         L.pft_comm_loopback_rank.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
         L.pft_comm_set_current.argtypes = [C.c_void_p]
         L.pft_comm_destroy.argtypes = [C.c_void_p]
+        L.pft_comm_set_self_exchange.argtypes = [C.c_void_p, C.c_int]
+        L.pft_comm_splits.argtypes = [C.c_void_p]
         L.pft_comm_barrier.argtypes = [C.c_void_p]
         L.pft_comm_current.restype = C.c_void_p
         L.pft_comm_kind.argtypes = [C.c_void_p]

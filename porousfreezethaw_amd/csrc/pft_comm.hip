@@ -36,6 +36,7 @@ struct pft_comm {
   hipEvent_t ev_ready, ev_done;
   int pending;
   void* dscratch;   // 256 bytes of device memory for host-level collectives
+  int self_x;       // diagnostic: 1-rank RCCL communicator exchanging with itself
 };
 
 static __thread pft_comm* g_current = nullptr;
@@ -154,6 +155,13 @@ int pft_comm_destroy(pft_comm* c)
 }
 
 int pft_comm_rank(const pft_comm* c) { return c ? c->rank : 0; }
+int pft_comm_splits(const pft_comm* c) { return c && (c->size > 1 || c->self_x); }
+int pft_comm_set_self_exchange(pft_comm* c, int on)
+{
+  if (!c || c->kind != KIND_RCCL || c->size != 1) return -2;
+  c->self_x = on ? 1 : 0;
+  return 0;
+}
 int pft_comm_size(const pft_comm* c) { return c ? c->size : 1; }
 const char* pft_comm_kind(const pft_comm* c)
 {
@@ -180,14 +188,17 @@ static void loop_barrier(pft_comm* c) { pthread_barrier_wait(&c->grp->bar); }
 
 int pft_comm_halo_start(pft_comm* c, int buf, int f0, int f1)
 {
-  if (!c || c->size == 1) return 0;
+  if (!pft_comm_splits(c)) return 0;
   pft_slab* s = c->slab;
   if (!s) return -2;
   hipStream_t st = (hipStream_t)pft_slab_stream(s);
   const size_t plane = pft_slab_plane(s), fs = pft_slab_field_stride(s);
   const int n3 = pft_slab_nz(s);
   double* b = pft_slab_buffer(s, buf);
-  const int below = c->rank > 0, above = c->rank < c->size - 1;
+  const int below = c->rank > 0 || c->self_x, above = c->rank < c->size - 1 || c->self_x;
+  // self exchange (diagnostic, one slab): the boundary planes go to the slab's own ghost planes,
+  // which a single slab never reads (mirror bottom wall, Dirichlet top)
+  const int pb = c->self_x ? c->rank : c->rank - 1, pa = c->self_x ? c->rank : c->rank + 1;
   if (c->kind == KIND_RCCL) {
     hipStream_t cs = (hipStream_t)pft_slab_comm_stream(s);
     HCHK(hipEventRecord(c->ev_ready, st));
@@ -196,12 +207,12 @@ int pft_comm_halo_start(pft_comm* c, int buf, int f0, int f1)
     for (int f = f0; f < f1; ++f) {
       double* fld = b + f * fs;
       if (below) {
-        NCCLCHK(ncclSend(fld + 1 * plane, plane, ncclFloat64, c->rank - 1, c->nccl, cs));
-        NCCLCHK(ncclRecv(fld + 0 * plane, plane, ncclFloat64, c->rank - 1, c->nccl, cs));
+        NCCLCHK(ncclSend(fld + 1 * plane, plane, ncclFloat64, pb, c->nccl, cs));
+        NCCLCHK(ncclRecv(fld + 0 * plane, plane, ncclFloat64, pb, c->nccl, cs));
       }
       if (above) {
-        NCCLCHK(ncclSend(fld + (size_t)n3 * plane, plane, ncclFloat64, c->rank + 1, c->nccl, cs));
-        NCCLCHK(ncclRecv(fld + (size_t)(n3 + 1) * plane, plane, ncclFloat64, c->rank + 1, c->nccl, cs));
+        NCCLCHK(ncclSend(fld + (size_t)n3 * plane, plane, ncclFloat64, pa, c->nccl, cs));
+        NCCLCHK(ncclRecv(fld + (size_t)(n3 + 1) * plane, plane, ncclFloat64, pa, c->nccl, cs));
       }
     }
     NCCLCHK(ncclGroupEnd());
@@ -233,7 +244,7 @@ int pft_comm_halo_start(pft_comm* c, int buf, int f0, int f1)
 
 int pft_comm_halo_finish(pft_comm* c)
 {
-  if (!c || c->size == 1 || !c->pending) return 0;
+  if (!pft_comm_splits(c) || !c->pending) return 0;
   c->pending = 0;
   HCHK(hipStreamWaitEvent((hipStream_t)pft_slab_stream(c->slab), c->ev_done, 0));
   return 0;
@@ -247,7 +258,7 @@ int pft_comm_halo(pft_comm* c, int buf, int f0, int f1)
 
 int pft_comm_allreduce_eps(pft_comm* c)
 {
-  if (!c || c->size == 1) return 0;
+  if (!pft_comm_splits(c)) return 0;
   pft_slab* s = c->slab;
   hipStream_t st = (hipStream_t)pft_slab_stream(s);
   unsigned long long* d = (unsigned long long*)pft_slab_scratch(s);

@@ -68,6 +68,9 @@
 #ifndef PFT_FUSED_WAVES
 #define PFT_FUSED_WAVES 3
 #endif
+#ifndef PFT_COMM_HIPRIO
+#define PFT_COMM_HIPRIO 1
+#endif
 #ifndef PFT_KUNROLL
 #define PFT_KUNROLL 1
 #endif
@@ -268,6 +271,7 @@ struct StageArgs {
   int n1, n2, n3, plane;
   int has_below, has_above;
   int k_begin, k_end, kz, ntile, nchunk;
+  int kspan;           // planes a chunk processes from its start (kz, or 1 for the boundary planes)
   double T_top;        // Dirichlet value T_top(t_stage), equation.c:110
   double coef, h;
   double em0, em1, em2;
@@ -324,7 +328,7 @@ __global__ __launch_bounds__(PFT_BLOCK) void merson_stage(StageArgs a, pft_const
   const int cc = active ? cell : a.plane - 1;
   const int j = cc / a.n1, i = cc - j * a.n1;
   const int kb = a.k_begin + chunk * a.kz;
-  const int ke = min(kb + a.kz, a.k_end);
+  const int ke = min(kb + a.kspan, a.k_end);
 
   // neighbour offsets within a plane, mirrored at the x/y walls (equation.c:137-161)
   const int oxm = i > 0 ? -1 : 0, oxp = i < a.n1 - 1 ? 1 : 0;
@@ -536,7 +540,7 @@ __global__ __launch_bounds__(PFT_BLOCK) void merson_tile(StageArgs a, pft_consts
   const bool active = (i0 < a.n1) && (j < a.n2);
   const long po = (long)(j < a.n2 ? j : a.n2 - 1) * a.n1 + (i0 < a.n1 ? i0 : a.n1 - 2);   // own pair
   const int kb = a.k_begin + chunk * a.kz;
-  const int ke = min(kb + a.kz, a.k_end);
+  const int ke = min(kb + a.kspan, a.k_end);
   const int lo = (ty + 1) * G::LW + 2 + 2 * tx;                                            // own pair in LDS
 
   // halo pair served by this thread (field hf, LDS index hl, plane offset hp)
@@ -771,7 +775,7 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
   const bool active = (i0 < a.n1) && (j < a.n2) && (int)threadIdx.x < WX * TY;
   const long po = (long)(j < a.n2 ? j : a.n2 - 1) * a.n1 + (i0 < a.n1 ? i0 : a.n1 - 2);
   const int kb = a.k_begin + chunk * a.kz;
-  const int ke = min(kb + a.kz, a.k_end);
+  const int ke = min(kb + a.kspan, a.k_end);
   const int lo = (ty + 1) * LW + 2 + 2 * tx;
 
   const int t = threadIdx.x;
@@ -1223,7 +1227,15 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
   s->recompute = 1;
   const size_t bytes = sizeof(double) * 3 * (size_t)s->fs;
   hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+#if PFT_COMM_HIPRIO
+  // the halo exchange's stream at the greatest priority: its RCCL kernel is dispatched ahead of
+  // the interior sweep's workgroups when both become ready
+  int prio_lo = 0, prio_hi = 0;
+  if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&s->comm, hipStreamNonBlocking, prio_hi);
+#else
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->comm, hipStreamNonBlocking);
+#endif
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&s->ev_eps, hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc((void**)&s->scratch, 64);
@@ -1488,6 +1500,13 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
 {
   const int mode = s->d.calc_mode;
   if (mode != 0 && mode != 1 && mode != 2 && mode != 10 && mode != 11) return -2;
+  // k_begin == PFT_K_BOUNDARY: the slab's two boundary planes (0 and n3 - 1) in ONE launch, two
+  // one-plane chunks n3 - 1 planes apart (what the z-neighbours need first)
+  const bool bnd = k_begin == PFT_K_BOUNDARY;
+  if (bnd) {
+    k_begin = 0;
+    k_end = s->d.n3;
+  }
   if (k_begin < 0) k_begin = 0;
   if (k_end < 0 || k_end > s->d.n3) k_end = s->d.n3;
   if (k_end <= k_begin) return 0;
@@ -1557,6 +1576,12 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
     a.kz = (nplanes + best_nch - 1) / best_nch;
   }
   a.nchunk = (nplanes + a.kz - 1) / a.kz;
+  a.kspan = a.kz;
+  if (bnd) {
+    a.kz = std::max(1, s->d.n3 - 1);
+    a.kspan = 1;
+    a.nchunk = s->d.n3 > 1 ? 2 : 1;
+  }
   a.T_top = t_stage < s->c.phase_switch_time ? s->c.top_temp1 : s->c.top_temp2;
   a.coef = coef;
   a.h = h;

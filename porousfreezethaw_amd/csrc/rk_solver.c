@@ -208,20 +208,20 @@ static int do_stage(int stage, double ts, double coef, double h, long * launches
 	const int tstage = stage == 6 ? 1 : stage;
 	int rc, n3;
 	if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 0);
-	if(pft_comm_size(c) == 1) {
+	if(!pft_comm_splits(c)) {
 		(*launches)++;
 		rc = run1(stage, ts, coef, h, -1, -1);
 		if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
 		return rc;
 	}
-	/* boundary planes first, their exchange overlaps the interior sweep */
+	/* both boundary planes first (one launch), their exchange overlaps the interior sweep
+	    */
 	n3 = R.slab_grid.n3;
-	if((rc = run1(stage, ts, coef, h, 0, 1))) return rc;
-	if(n3 > 1 && (rc = run1(stage, ts, coef, h, n3-1, n3))) return rc;
+	if((rc = run1(stage, ts, coef, h, PFT_K_BOUNDARY, 0))) return rc;
 	if((rc = pft_comm_halo_start(c, out_buf, 0, nfields))) return rc;
 	if(n3 > 2 && (rc = run1(stage, ts, coef, h, 1, n3-1))) return rc;
 	if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
-	*launches += 3;
+	*launches += 2;
 	return pft_comm_halo_finish(c);
 }
 
