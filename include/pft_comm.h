@@ -66,6 +66,10 @@ int pft_comm_halo_finish(pft_comm * c);
 int pft_comm_halo(pft_comm * c, int buf, int f0, int f1);   /* start + finish */
 /* eps max over ranks, on the slab's scratch (u64 bits + non-finite flag), stream-ordered */
 int pft_comm_allreduce_eps(pft_comm * c);
+/* eps max over ranks + its publication to pinned host memory (pft_slab_eps_mark): with RCCL both
+   run on the communication stream, off the compute stream's critical path (the speculative
+   stage 1 is enqueued right after); a single rank just publishes */
+int pft_comm_eps_publish(pft_comm * c);
 /* host-level collectives used outside the per-stage path */
 int pft_comm_bcast(pft_comm * c, void * data, int bytes, int root);
 int pft_comm_allreduce_max_i64(pft_comm * c, long long * v);

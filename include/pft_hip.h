@@ -140,6 +140,9 @@ int pft_slab_swap_buffers(pft_slab * s, int a, int b);
 int pft_slab_can_speculate(const pft_slab * s);
 int pft_slab_stage_spec(pft_slab * s, double t_stage, int k_begin, int k_end);
 int pft_slab_eps_mark(pft_slab * s);
+/* the same publication enqueued on another stream of the slab's device (the communication
+   stream, behind the eps max over ranks: pft_comm_eps_publish) */
+int pft_slab_eps_mark_on(pft_slab * s, void * stream);
 
 /* generic chunk-table combines for the host-staged path (any RK_MEM_DIST on a flat array) */
 int pft_flat_alloc(double ** p, size_t n);

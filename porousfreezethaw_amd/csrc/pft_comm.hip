@@ -286,6 +286,25 @@ int pft_comm_allreduce_eps(pft_comm* c)
   return 0;
 }
 
+int pft_comm_eps_publish(pft_comm* c)
+{
+  if (!c || !c->slab) return -2;
+  pft_slab* s = c->slab;
+  if (!pft_comm_splits(c)) return pft_slab_eps_mark(s);
+  if (c->kind == KIND_RCCL) {
+    // the max over ranks and the publication run on the communication stream, so the compute
+    // stream goes on with the speculative stage 1 while RCCL reduces
+    hipStream_t st = (hipStream_t)pft_slab_stream(s), cs = (hipStream_t)pft_slab_comm_stream(s);
+    unsigned long long* d = (unsigned long long*)pft_slab_scratch(s);
+    HCHK(hipEventRecord(c->ev_ready, st));
+    HCHK(hipStreamWaitEvent(cs, c->ev_ready, 0));
+    NCCLCHK(ncclAllReduce(d, d, 2, ncclUint64, ncclMax, c->nccl, cs));
+    return pft_slab_eps_mark_on(s, (void*)cs);
+  }
+  const int rc = pft_comm_allreduce_eps(c);
+  return rc ? rc : pft_slab_eps_mark(s);
+}
+
 int pft_comm_bcast(pft_comm* c, void* data, int bytes, int root)
 {
   if (!c || c->size == 1) return 0;

@@ -1662,15 +1662,17 @@ int pft_slab_eps_reset(pft_slab* s)
   return 0;
 }
 
-int pft_slab_eps_mark(pft_slab* s)
+int pft_slab_eps_mark(pft_slab* s) { return pft_slab_eps_mark_on(s, (void*)s->stream); }
+
+int pft_slab_eps_mark_on(pft_slab* s, void* stream)
 {
   // the error norm goes to coherent pinned host memory by a one-thread kernel (which also resets
   // it for the next step), and an event marks its completion: the host waits for that event
   // only, never for a copy queued behind (or beside) the speculative stage-1 kernel that follows
   // on the compute stream
-  publish_kernel<<<1, 1, 0, s->stream>>>(s->scratch, s->host_pub_dev);
+  publish_kernel<<<1, 1, 0, (hipStream_t)stream>>>(s->scratch, s->host_pub_dev);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(s->ev_eps, s->stream));
+  HIPCHK(hipEventRecord(s->ev_eps, (hipStream_t)stream));
   s->eps_marked = 1;
   return 0;
 }

@@ -273,11 +273,11 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 		if((rc = do_stage(3, t+h3, h8, h, &launches))) return rc;    /* :412-429 */
 		if((rc = do_stage(4, t+h2, h,  h, &launches))) return rc;    /* :432-450 */
 		if((rc = do_stage(5, t+h,  h3, h, &launches))) return rc;    /* :453,507-524,657-668 */
-		if((rc = pft_comm_allreduce_eps(c))) return rc;                          /* :572 */
 		if(spec) {
-			if((rc = pft_slab_eps_mark(R.slab))) return rc;
+			/* eps max over ranks (:572) and its publication beside the speculative stage 1 */
+			if((rc = pft_comm_eps_publish(c))) return rc;
 			if((rc = do_stage(6, t+h, 0.0, h, &launches))) return rc;
-		}
+		} else if((rc = pft_comm_allreduce_eps(c))) return rc;                  /* :572 */
 		if((rc = pft_slab_eps_fetch(R.slab, &eps, &nonfinite))) return rc;
 		if(R.opt_timing) pft_slab_timing_collect(R.slab, R.stats.stage_ms, R.stats.stage_n);
 		system->steps_total++;                                                   /* :460 */
