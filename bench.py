@@ -201,7 +201,7 @@ def main():
         if os.path.exists(pmc):
             try:
                 ps = json.load(open(pmc))
-                key = f"stage{dom}_gl{int(a.gl_static)}_g{gn}_n{world}_m{a.mode}"
+                key = f"stage{dom}_gl{int(a.gl_static)}_{n1}x{n2}x{sim.grid.n3}_m{a.mode}"
                 traffic = ps.get(key, {}).get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None

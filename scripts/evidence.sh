@@ -22,11 +22,19 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof/trace -o run --out
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $O/prof/fetch -o run --output-format csv -- python3 bench.py $ARGS > $O/prof/fetch_bench.json 2> $O/prof/fetch.err; fatal $? fetch
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $O/prof/write -o run --output-format csv -- python3 bench.py $ARGS > $O/prof/write_bench.json 2> $O/prof/write.err; fatal $? write
 PB=$(python3 -c "import json;print(json.load(open('$O/prof/trace_bench.json'))['probe_bytes_each_way'])")
-python3 scripts/pmc_summary.py $O/prof/trace $O/prof/fetch $O/prof/write 400 $PB $O/pmc_summary.json > $O/pmc_summary.txt 2>&1; fatal $? pmc_summary
+python3 scripts/pmc_summary.py $O/prof/trace $O/prof/fetch $O/prof/write 200x200x400 $PB $O/pmc_summary.json > $O/pmc_summary.txt 2>&1; fatal $? pmc_summary
 cp $O/pmc_summary.json profiles/pmc_summary.json
 timeout -k 10 900 python bench.py > $O/bench_default.json 2> $O/bench_default.err; fatal $? bench_default
 timeout -k 10 300 python bench.py --steps 100 --no-cpu --mode 1 > $O/bench_mode1.json 2>> $O/bench_var.err; fatal $? bench_mode1
 timeout -k 10 300 python bench.py --steps 100 --no-cpu --mode 2 > $O/bench_mode2.json 2>> $O/bench_var.err; fatal $? bench_mode2
 timeout -k 10 300 python bench.py --steps 100 --no-cpu --gl-static > $O/bench_gls.json 2>> $O/bench_var.err; fatal $? bench_gls
 timeout -k 10 600 python bench.py --steps 50 --no-cpu --literal-cube > $O/bench_cube64M.json 2>> $O/bench_var.err; fatal $? bench_cube
+# per-rank slabs of the N > 1 cube workloads on one GPU, plain and through the RCCL stage
+# pipeline with a self-exchanging 1-rank communicator (--self-exchange)
+for dom in "400 0.06,0.06,0.015 n8" "318 0.06,0.06,0.03 n4" "252 0.06,0.06,0.06 n2"; do
+  set -- $dom
+  timeout -k 10 300 python bench.py --steps 100 --no-cpu --grid-nodes $1 --domain $2 > $O/bench_slab_$3.json 2>> $O/bench_var.err; fatal $? slab_$3
+  timeout -k 10 300 python bench.py --steps 100 --no-cpu --grid-nodes $1 --domain $2 --self-exchange > $O/bench_slab_$3_selfx.json 2>> $O/bench_var.err; fatal $? slab_$3_selfx
+done
+timeout -k 10 300 python bench.py --steps 100 --no-cpu --self-exchange > $O/bench_selfx.json 2>> $O/bench_var.err; fatal $? bench_selfx
 echo done >> $O/status.log

@@ -6,7 +6,7 @@ runs (FETCH_SIZE, WRITE_SIZE -- separate passes, MI355X_MICROARCH.md "rocprofv3 
 Corrections (MI355X_MICROARCH.md "HBM"): FETCH_SIZE/WRITE_SIZE are in KiB; gfx950's FETCH_SIZE
 is only exact for calibrated access widths, so the ratio known/measured of the probe_copy_kernel
 (8-byte loads and stores per lane, exactly the stage kernels' width, known byte count) calibrates
-both counters.  Output keys: stage<k>_gl<0|1>_g<grid>_n1_m<mode> -> HBM bytes per launch.
+both counters.  Output keys: stage<k>_gl<0|1>_<n1>x<n2>x<n3>_m<mode> (the slab's cells) -> HBM bytes per launch.
 """
 import csv
 import glob
@@ -43,7 +43,7 @@ def kname(k):
     return None, None, None
 
 
-def main(trace_dir, fetch_dir, write_dir, grid, probe_bytes, out_path):
+def main(trace_dir, fetch_dir, write_dir, dims, probe_bytes, out_path):
     fetch, write = counters(fetch_dir, "FETCH_SIZE"), counters(write_dir, "WRITE_SIZE")
     pf = [v for k, v in fetch.items() if kname(k)[0] == "probe"]
     pw = [v for k, v in write.items() if kname(k)[0] == "probe"]
@@ -62,7 +62,7 @@ def main(trace_dir, fetch_dir, write_dir, grid, probe_bytes, out_path):
             continue
         fb = fetch.get(k, 0.0) * 1024 * cal_f
         wb = write.get(k, 0.0) * 1024 * cal_w
-        key = f"{st}_gl{int(gls)}_g{grid}_n1_m{mode}"
+        key = f"{st}_gl{int(gls)}_{dims}_m{mode}"
         res[key] = {"kernel": k, "fetch_bytes": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
                     "raw_FETCH_SIZE_KiB": fetch.get(k), "raw_WRITE_SIZE_KiB": write.get(k)}
     res["kernel_stats"] = stats
@@ -72,4 +72,4 @@ def main(trace_dir, fetch_dir, write_dir, grid, probe_bytes, out_path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5]), sys.argv[6])
+    main(sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), sys.argv[6])
