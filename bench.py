@@ -184,6 +184,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     stats = sim.stats()
+    geo = sim.tile_geometry()
 
     # ---- roofline: dominant fused stage kernel, HIP events on the slab's compute stream -----
     roof = None
@@ -241,7 +242,9 @@ def main():
                    "calc_mode": a.mode, "cells": cells_total, "parallelism": f"zslab{world}",
                    "gl_static": a.gl_static, "kz": a.kz or "auto", "tile": a.tile, "recompute": not a.no_recompute,
                    "accepted_steps_total": int(sim.system.steps), "t_end": sim.t,
-                   "host_boundary": a.host_boundary, "self_exchange": a.self_exchange},
+                   "host_boundary": a.host_boundary, "self_exchange": a.self_exchange,
+                   "tiles": ({str(k): ("cache" if v[0] == 0 else f"{2 * v[1]}x{v[2]} cells")
+                              for k, v in geo.items()} if geo else None)},
         "roofline": roof,
         "fused_effective_GBps": round(step_bytes * cells_total * steps / el / 1e9 / world, 1),
         "survey_840B_equiv_GBps": round(SURVEY_BYTES_PER_CELL_STEP * cells_total * steps / el / 1e9 / world, 1),

@@ -77,9 +77,14 @@ const pft_slab_desc * pft_slab_get_desc(const pft_slab * s);
    workgroup that keep the whole launch resident in one round (occupancy x CUs / tiles chunks) */
 int pft_slab_set_kz(pft_slab * s, int kz);
 /* stage kernel flavour: 32 or 16 = LDS-tiled kernel with 64x8 / 32x16 cell tiles (n1 even);
-   1 (default) = per stage (32x16 for the VALU-bound stages 1-2, 64x8 for 3-5); 0 = cache-based
-   kernel (any n1; also used automatically for odd n1) */
+   1 (default) = automatic: the cache kernel for slabs too small to fill the GPU with tiles, else
+   the fused kernel with a tile fitted to n1 x n2 (the aux-array kernel: 32x16 for stages 1-2,
+   64x8 for 3-5); 2 = as 1 at any slab size; 0 = cache-based kernel (any n1; also used
+   automatically for odd n1) */
 int pft_slab_set_tile(pft_slab * s, int wx);
+/* the kernel flavour (0 cache, 1 LDS tile with aux arrays, 2 fused recompute) and tile (wx cell
+   pairs x ty rows; 0 x 0 for the cache kernel) that stage 1..5 launches on this slab */
+int pft_slab_tile_geometry(const pft_slab * s, int stage, int * wx, int * ty);
 /* 1 (default): the tiled kernels rebuild every stage input from x and the K's inside the
    stencil (no aux arrays: 54 instead of 72 doubles of traffic per cell-step, bit-identical);
    0: the reference's aux arrays are materialised between stages */

@@ -36,8 +36,9 @@ enum {
 	PFT_OPT_TIMING = 4,     /* N > 0: time the stages of every N-th attempted step with HIP events
 	                           (stats.stage_ms / stage_n); each timed stage adds ~3 us of
 	                           event-packet overhead, so benchmarks sample (N = 10) */
-	PFT_OPT_TILE = 5,       /* stage kernel: 1 (default) = per stage, 32 / 16 = LDS-tiled 64x8 /
-	                           32x16 tiles, 0 = cache-based kernel (pft_slab_set_tile) */
+	PFT_OPT_TILE = 5,       /* stage kernel: 1 (default) = automatic, 2 = LDS-tiled at any size with
+	                           the automatic tile, 32 / 16 = LDS-tiled 64x8 / 32x16 tiles, 0 =
+	                           cache-based kernel (pft_slab_set_tile) */
 	PFT_OPT_RECOMPUTE = 6   /* 1 (default): rebuild stage inputs from x and the K's inside the
 	                           stencil, 0: materialise the aux arrays (pft_slab_set_recompute) */
 };

@@ -98,6 +98,7 @@ def lib():
         L.pft_solver_set_option.argtypes = [C.c_int, C.c_long]
         L.pft_solver_get_stats.argtypes = [C.POINTER(pft_solver_stats)]
         L.pft_solver_slab.restype = C.c_void_p
+        L.pft_slab_tile_geometry.argtypes = [C.c_void_p, C.c_int, ip, ip]
         L.pft_decompose.argtypes = [C.c_int, C.c_int, C.c_int, ip, ip]
         L.pft_decompose.restype = None
         L.pft_grid_init.argtypes = [C.POINTER(pft_grid), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -282,6 +283,19 @@ class Simulation:
         rc = self.lib.pft_solver_download(C.byref(self.system))
         if rc:
             raise RuntimeError(f"pft_solver_download failed ({rc})")
+
+    def tile_geometry(self):
+        """{stage: (kernel kind, wx cell pairs, ty rows)} of the slab's stage launches (kind 0 cache,
+        1 LDS tile with aux arrays, 2 fused recompute); the slab exists after the first solve"""
+        slab = self.lib.pft_solver_slab()
+        if not slab:
+            return None
+        out = {}
+        for st in range(1, 6):
+            wx, ty = C.c_int(), C.c_int()
+            kind = self.lib.pft_slab_tile_geometry(slab, st, C.byref(wx), C.byref(ty))
+            out[st] = (kind, wx.value, ty.value)
+        return out
 
     def stats(self):
         s = pft_solver_stats()

@@ -1173,7 +1173,8 @@ struct pft_slab {
   int kz;                // planes per workgroup z-march; 0 = automatic (one full round, see auto_kz)
   int n_cu;               // compute units of the slab's device
   double* noise;         // device u_noise (n3*plane) or null
-  int tile_wx;           // 32 / 16: LDS-tiled kernels with that many threads per row; 1: per stage; 0: cache-based
+  int tile_wx;           // 32 / 16: LDS-tiled kernels with that many pairs per row; 1: automatic;
+                         // 2: LDS-tiled at any size, automatic tile; 0: cache-based
   int n1_tiled_ok;
   int recompute;         // 1: stage inputs rebuilt from x and the K's (no aux arrays)
   // per-stage timing: a ring of begin/end event pairs, so that kernels still running when the
@@ -1293,7 +1294,7 @@ void* pft_slab_scratch(pft_slab* s) { return (void*)s->scratch; }
 const pft_slab_desc* pft_slab_get_desc(const pft_slab* s) { return &s->d; }
 int pft_slab_set_tile(pft_slab* s, int wx)
 {
-  if (wx != 0 && wx != 1 && wx != 16 && wx != 32) return -2;
+  if (wx != 0 && wx != 1 && wx != 2 && wx != 16 && wx != 32) return -2;
   s->tile_wx = wx;
   return 0;
 }
@@ -1449,16 +1450,6 @@ int pft_slab_stage_output(const pft_slab* s, int stage)
   return slab_kind(s) == KFUSED ? rc_out[stage] : aux_out[stage];
 }
 
-int pft_slab_stage_fields(const pft_slab* s, int stage)
-{
-  // fields of a stage's output buffer that the stage writes (stage 6: the speculative stage 1):
-  // gl is not evolved under gl_static, and its K's are literal zeros on the recompute path
-  if (stage < 1 || stage > 6) return -2;
-  if (s->d.gl_static) return 2;
-  if (slab_kind(s) == KFUSED && PFT_GLK_LITERAL && stage != 5) return 2;
-  return 3;
-}
-
 // merson_fused tile: wx cell pairs x ty rows, 256 threads.  Limits: wx * ty <= 256 threads, the
 // halo ring (2 wx + 4 + 2 ty pairs per field, 3 fields) loaded by one pass of the 256 threads,
 // (2 wx + 4)(ty + 2) <= PFT_FUSED_LF doubles of LDS per field and plane.
@@ -1493,6 +1484,32 @@ static void fused_geometry(int n1, int n2, int* wx_out, int* ty_out)
   }
   *wx_out = bw;
   *ty_out = bt;
+}
+
+int pft_slab_tile_geometry(const pft_slab* s, int stage, int* wx, int* ty)
+{
+  const int kind = slab_kind(s);
+  const bool auto_tile = s->tile_wx == 1 || s->tile_wx == 2;
+  if (kind == KCACHE) {
+    *wx = 0;
+    *ty = 0;
+  } else if (kind == KFUSED && auto_tile) {
+    fused_geometry(s->d.n1, s->d.n2, wx, ty);
+  } else {
+    *wx = auto_tile ? (stage <= 2 ? 16 : 32) : s->tile_wx;
+    *ty = PFT_BLOCK / *wx;
+  }
+  return kind;
+}
+
+int pft_slab_stage_fields(const pft_slab* s, int stage)
+{
+  // fields of a stage's output buffer that the stage writes (stage 6: the speculative stage 1):
+  // gl is not evolved under gl_static, and its K's are literal zeros on the recompute path
+  if (stage < 1 || stage > 6) return -2;
+  if (s->d.gl_static) return 2;
+  if (slab_kind(s) == KFUSED && PFT_GLK_LITERAL && stage != 5) return 2;
+  return 3;
 }
 
 static int run_stage(pft_slab* s, int stage, const double* in, double* kout, double* out, double t_stage,
@@ -1534,9 +1551,10 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   a.k_end = k_end;
   // tile width: 1 = per stage (measured at 400^3: the VALU-bound stages 0-2 run faster on 32x16
   // tiles -- fewer idle lanes at the x edge, 200 = 6.25 x 32 -- the HBM-bound stages 3-5 on 64x8)
-  const int wx = kind == KCACHE ? 0 : s->tile_wx == 1 ? (stage <= 2 ? 16 : 32) : s->tile_wx;
+  const bool auto_tile = s->tile_wx == 1 || s->tile_wx == 2;
+  const int wx = kind == KCACHE ? 0 : auto_tile ? (stage <= 2 ? 16 : 32) : s->tile_wx;
   if (kind == KFUSED) {
-    if (s->tile_wx == 1) {
+    if (auto_tile) {
       fused_geometry(s->d.n1, s->d.n2, &a.gwx, &a.gty);
     } else {
       a.gwx = s->tile_wx;

@@ -124,7 +124,7 @@ int pft_solver_set_option(int opt, long value)
 		case PFT_OPT_RECOMPUTE:
 			R.opt_norecompute = value ? 0 : 1; if(R.slab) pft_slab_set_recompute(R.slab, !R.opt_norecompute); return 0;
 		case PFT_OPT_TILE:
-			if(value != 0 && value != 16 && value != 32) return -2;
+			if(value != 0 && value != 1 && value != 2 && value != 16 && value != 32) return -2;
 			R.opt_tile = (int)value; if(R.slab) pft_slab_set_tile(R.slab, R.opt_tile); return 0;
 	}
 	return -2;

@@ -24,7 +24,8 @@ def need_gpu():
 
 # kernel flavours: (tile width, recompute stage inputs)
 FLAVOURS = {"cache": (0, False), "tile32": (32, False), "tile16": (16, False),
-            "fused32": (32, True), "fused16": (16, True), "default": (1, True)}
+            "fused32": (32, True), "fused16": (16, True), "default": (1, True),
+            "fusedauto": (2, True)}   # the fused kernel with the tile fitted to n1 x n2, at any size
 
 
 def make_sim(meta, initial, mode=None, flavour=None, **kw):
@@ -120,13 +121,20 @@ def test_step_limited_resident_equals_continuous():
     sim.close()
 
 
+# fusedauto grids and the tile fused_geometry picks (wx pairs x ty rows): 50x50 -> 25x10 (exact),
+# 252x14 -> 18x14, 318x10 -> 25x10 (partial x tile), 130x70 and 66x38 -> 33x7 (one tile wide),
+# 100x36 -> 28x9
 @pytest.mark.parametrize("dims,flavour", [((30, 30, 60), "fused32"), ((30, 30, 60), "fused16"),
                                           ((66, 38, 21), "fused32"), ((17, 9, 13), "fused32"),
                                           ((130, 70, 9), "fused16"), ((66, 38, 21), "tile32"),
-                                          ((130, 70, 9), "cache")])
+                                          ((130, 70, 9), "cache"), ((50, 50, 20), "fusedauto"),
+                                          ((252, 14, 6), "fusedauto"), ((318, 10, 5), "fusedauto"),
+                                          ((130, 70, 9), "fusedauto"), ((66, 38, 21), "fusedauto"),
+                                          ((100, 36, 12), "fusedauto")])
 def test_matches_oracle_larger_grid(dims, flavour):
     """default Params on several grids (odd n1 falls back to the cache-based kernel; tiles with
-    partial x/y coverage), from the default IC, 12 attempted steps vs the oracle"""
+    partial x/y coverage; automatic tiles of any width), from the default IC, 12 attempted steps
+    vs the oracle"""
     meta, A = O.load_case("g20")
     Pm, info = O.params_from_meta(meta)
     n1, n2, n3 = dims
@@ -197,6 +205,70 @@ def test_multislab_loopback_bitwise(nprocs, gl_static, flavour):
             assert (t, s, st, rc) == (float.fromhex(ref[0]), ref[2], ref[3], ref[4])
         full = np.concatenate([out[r][i][5] for r in range(nprocs)], axis=1)
         assert np.array_equal(full, A[f"traj_m0_state{i}"])
+
+
+def _self_exchange_comm():
+    L = P.lib()
+    uid = (C.c_char * 128)()
+    assert L.pft_comm_get_unique_id(uid) == 0
+    comm = C.c_void_p()
+    assert L.pft_comm_init_rccl(C.byref(comm), 1, 0, uid, 0) == 0
+    assert L.pft_comm_set_self_exchange(comm, 1) == 0
+    assert L.pft_comm_splits(comm) == 1
+    return comm
+
+
+@pytest.mark.parametrize("gl_static", [False, True])
+@pytest.mark.parametrize("flavour", ["default", "fusedauto", "fused16", "tile32", "cache"])
+def test_rccl_stage_pipeline_self_exchange_bitwise(gl_static, flavour):
+    """the N > 1 stage pipeline through real RCCL calls on one GPU (pft_comm_set_self_exchange):
+    both boundary planes in one launch, ncclSend/ncclRecv on the priority comm stream beside the
+    interior sweep, the eps max by ncclAllReduce and its publication on the comm stream.  The
+    exchanged planes land in the slab's own ghost planes, which one slab never reads, so the
+    trajectory must equal the reference's bit for bit"""
+    L = P.lib()
+    comm = _self_exchange_comm()
+    L.pft_comm_set_current(comm)
+    try:
+        meta, A = O.load_case("g20")
+        sim, Pm, info = make_sim(meta, A["traj_m0_ic"], mode=0, gl_static=gl_static, flavour=flavour)
+        for i, T in enumerate(meta["traj_times"][:2]):
+            rc = sim.solve(T)
+            ref = meta["traj_m0"][i]
+            assert (sim.t.hex(), sim.h.hex(), sim.system.steps, sim.system.steps_total, rc) == \
+                (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(), ref[2], ref[3], ref[4])
+            assert np.array_equal(sim.interior(), A[f"traj_m0_state{i}"])
+        sim.close()
+    finally:
+        L.pft_comm_set_current(None)
+        L.pft_comm_destroy(comm)
+
+
+def test_rccl_stage_pipeline_self_exchange_larger_grid():
+    """the same pipeline on a 100 x 36 x 40 grid with the automatic fused tile (several z-chunks,
+    boundary launch of two one-plane chunks) vs the oracle, 12 attempted steps"""
+    L = P.lib()
+    comm = _self_exchange_comm()
+    L.pft_comm_set_current(comm)
+    try:
+        meta, A = O.load_case("g20")
+        Pm, info = O.params_from_meta(meta)
+        n1, n2, n3 = 100, 36, 40
+        info = dict(info, n1=n1, n2=n2, n3=n3)
+        sim = P.Simulation(n1, n2, n3, (info["L1"], info["L2"], info["L3"]), 0, Pm, beads=O.beads(), tau=1.0,
+                           tau_min=info["tau_min"], delta=info["delta"], tile=2)
+        ic = sim.interior()
+        assert sim.solve_ex(1e9, 12, 0) == 2
+        assert sim.stats().kernel_launches > 0
+        res = O.solve(info, Pm, 0, ic, 0.0, 1.0, [1e9], max_steps_total=12)[0]
+        assert (sim.t, sim.h, sim.system.steps, sim.system.steps_total) == (res[0], res[1], res[2], res[3])
+        assert np.array_equal(sim.interior(), res[5])
+        geo = sim.tile_geometry()
+        assert geo[5] == (2, 28, 9)      # fused kernel, fused_geometry's tile for 100 x 36
+        sim.close()
+    finally:
+        L.pft_comm_set_current(None)
+        L.pft_comm_destroy(comm)
 
 
 def test_host_staged_path_with_foreign_rhs():
