@@ -1431,25 +1431,6 @@ static void launch_stage(int stage, int mode, int kind, int wx, dim3 g, hipStrea
 
 extern "C" {
 
-static int slab_kind(const pft_slab* s)
-{
-  if (s->d.n1 % 2 != 0 || s->tile_wx == 0) return KCACHE;   // 16-byte rows need n1 even
-  // automatic choice: a slab too small to fill the GPU with 512-cell tiles even one plane deep is
-  // latency-bound, and the cache kernel's 256-cell workgroups without LDS staging finish sooner
-  // (measured: 100^3, 250 k cells: 4 300 vs 3 700 Mcells*steps/s; 200^3, 2 M cells: 7 760 vs 9 040)
-  if (s->tile_wx == 1 && (long)s->plane * s->d.n3 < 4L * s->n_cu * 3 * 512) return KCACHE;
-  return s->recompute ? KFUSED : KTILE;
-}
-
-int pft_slab_stage_output(const pft_slab* s, int stage)
-{
-  // the buffer each stage of the step writes (and whose boundary planes neighbours need)
-  static const int aux_out[6] = {-1, PFT_BUF_A0, PFT_BUF_A1, PFT_BUF_A0, PFT_BUF_A1, PFT_BUF_XN};
-  static const int rc_out[6] = {-1, PFT_BUF_K1, PFT_BUF_A0 /* K2 */, PFT_BUF_K3, PFT_BUF_K4, PFT_BUF_XN};
-  if (stage < 1 || stage > 5) return -2;
-  return slab_kind(s) == KFUSED ? rc_out[stage] : aux_out[stage];
-}
-
 // merson_fused tile: wx cell pairs x ty rows, 256 threads.  Limits: wx * ty <= 256 threads, the
 // halo ring (2 wx + 4 + 2 ty pairs per field, 3 fields) loaded by one pass of the 256 threads,
 // (2 wx + 4)(ty + 2) <= PFT_FUSED_LF doubles of LDS per field and plane.
@@ -1465,7 +1446,7 @@ static bool fused_geometry_ok(int wx, int ty)
 // quarter of the workgroups are 7/8 idle; a z-march of 64-wide tiles streams at 4.7-4.9 TB/s
 // there and at 5.2-5.4 TB/s when n1 is a multiple of 64 (scripts/probes/stream_probe.hip).
 // n1 = 200 and 400: 25 x 10 pairs (50 x 10 cells), all lanes but 6 busy.
-static void fused_geometry(int n1, int n2, int* wx_out, int* ty_out)
+static double fused_geometry(int n1, int n2, int* wx_out, int* ty_out)
 {
   const int np = n1 / 2;
   double best = -1.0;
@@ -1484,6 +1465,32 @@ static void fused_geometry(int n1, int n2, int* wx_out, int* ty_out)
   }
   *wx_out = bw;
   *ty_out = bt;
+  return best;   // busy lanes / launched lanes over the plane
+}
+
+static int slab_kind(const pft_slab* s)
+{
+  if (s->d.n1 % 2 != 0 || s->tile_wx == 0) return KCACHE;   // 16-byte rows need n1 even
+  // automatic choice: the LDS-tiled kernels unless their tiles leave most lanes idle (planes
+  // narrower than a tile, e.g. n1 < 32); the cache kernel's flat 256-cell workgroups fit any
+  // plane.  Measured at 100^3 (50 x 50 x 100, 25 x 10-pair tiles fit exactly): 4 810 vs 3 980
+  // Mcells*steps/s (47 vs 60 us per attempted step untimed)
+  if (s->tile_wx == 1 && s->recompute) {
+    int wx, ty;
+    if (fused_geometry(s->d.n1, s->d.n2, &wx, &ty) < 0.7) return KCACHE;
+  } else if (s->tile_wx == 1 && (long)s->plane * s->d.n3 < 4L * s->n_cu * 3 * 512) {
+    return KCACHE;   // aux-array path, 64 x 8 / 32 x 16 tiles: the former size rule
+  }
+  return s->recompute ? KFUSED : KTILE;
+}
+
+int pft_slab_stage_output(const pft_slab* s, int stage)
+{
+  // the buffer each stage of the step writes (and whose boundary planes neighbours need)
+  static const int aux_out[6] = {-1, PFT_BUF_A0, PFT_BUF_A1, PFT_BUF_A0, PFT_BUF_A1, PFT_BUF_XN};
+  static const int rc_out[6] = {-1, PFT_BUF_K1, PFT_BUF_A0 /* K2 */, PFT_BUF_K3, PFT_BUF_K4, PFT_BUF_XN};
+  if (stage < 1 || stage > 5) return -2;
+  return slab_kind(s) == KFUSED ? rc_out[stage] : aux_out[stage];
 }
 
 int pft_slab_tile_geometry(const pft_slab* s, int stage, int* wx, int* ty)
