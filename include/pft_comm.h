@@ -63,6 +63,10 @@ int pft_comm_attach(pft_comm * c, pft_slab * s);
    No-ops for a single rank. */
 int pft_comm_halo_start(pft_comm * c, int buf, int f0, int f1);
 int pft_comm_halo_finish(pft_comm * c);
+/* the exchange enqueued on the slab's communication stream behind the work already there (the
+   boundary planes of the two-stream stage pipeline, rk_solver.c do_stage): nothing to finish,
+   later work on the comm stream follows it in stream order */
+int pft_comm_halo_enqueue_comm(pft_comm * c, int buf, int f0, int f1);
 int pft_comm_halo(pft_comm * c, int buf, int f0, int f1);   /* start + finish */
 /* eps max over ranks, on the slab's scratch (u64 bits + non-finite flag), stream-ordered */
 int pft_comm_allreduce_eps(pft_comm * c);

@@ -97,6 +97,16 @@ int pft_slab_stage_output(const pft_slab * s, int stage);
    path, where gl's K's are the literal zeros of dgl (equation.c:731) and never stored */
 int pft_slab_stage_fields(const pft_slab * s, int stage);
 
+/* N > 1 stage pipeline on two streams: stage launches go to the comm stream while `on` is set
+   (the boundary planes, then their exchange, beside the interior sweep on the compute stream);
+   pft_slab_order(s, 0): the comm stream waits for the compute stream's work so far, (s, 1): the
+   compute stream waits for the comm stream's */
+int pft_slab_launch_on_comm(pft_slab * s, int on);
+int pft_slab_order(pft_slab * s, int comm_first);
+/* wait = 0: mark the boundary launch just enqueued on the comm stream; wait = 1: the compute
+   stream waits for the last marked boundary launch (not for anything enqueued after it) */
+int pft_slab_boundary_event(pft_slab * s, int wait);
+
 /* host layout (reference padded, ghost thickness 2) <-> device layout, on the compute stream */
 int pft_slab_upload_host(pft_slab * s, int which, const double * host_padded);
 int pft_slab_download_host(pft_slab * s, int which, double * host_padded);

@@ -186,12 +186,14 @@ int pft_comm_attach(pft_comm* c, pft_slab* s)
 
 static void loop_barrier(pft_comm* c) { pthread_barrier_wait(&c->grp->bar); }
 
-int pft_comm_halo_start(pft_comm* c, int buf, int f0, int f1)
+static int halo_start(pft_comm* c, int buf, int f0, int f1, bool on_comm)
 {
   if (!pft_comm_splits(c)) return 0;
   pft_slab* s = c->slab;
   if (!s) return -2;
-  hipStream_t st = (hipStream_t)pft_slab_stream(s);
+  // on_comm: the boundary planes were written on the comm stream itself (two-stream stage
+  // pipeline), so the exchange follows them in stream order with no handshake
+  hipStream_t st = (hipStream_t)(on_comm ? pft_slab_comm_stream(s) : pft_slab_stream(s));
   const size_t plane = pft_slab_plane(s), fs = pft_slab_field_stride(s);
   const int n3 = pft_slab_nz(s);
   double* b = pft_slab_buffer(s, buf);
@@ -201,8 +203,10 @@ int pft_comm_halo_start(pft_comm* c, int buf, int f0, int f1)
   const int pb = c->self_x ? c->rank : c->rank - 1, pa = c->self_x ? c->rank : c->rank + 1;
   if (c->kind == KIND_RCCL) {
     hipStream_t cs = (hipStream_t)pft_slab_comm_stream(s);
-    HCHK(hipEventRecord(c->ev_ready, st));
-    HCHK(hipStreamWaitEvent(cs, c->ev_ready, 0));
+    if (!on_comm) {
+      HCHK(hipEventRecord(c->ev_ready, st));
+      HCHK(hipStreamWaitEvent(cs, c->ev_ready, 0));
+    }
     NCCLCHK(ncclGroupStart());
     for (int f = f0; f < f1; ++f) {
       double* fld = b + f * fs;
@@ -216,8 +220,10 @@ int pft_comm_halo_start(pft_comm* c, int buf, int f0, int f1)
       }
     }
     NCCLCHK(ncclGroupEnd());
-    HCHK(hipEventRecord(c->ev_done, cs));
-    c->pending = 1;
+    if (!on_comm) {
+      HCHK(hipEventRecord(c->ev_done, cs));
+      c->pending = 1;
+    }
     return 0;
   }
   // loopback: pull the neighbours' boundary planes into our ghost planes
@@ -241,6 +247,9 @@ int pft_comm_halo_start(pft_comm* c, int buf, int f0, int f1)
   loop_barrier(c);
   return 0;
 }
+
+int pft_comm_halo_start(pft_comm* c, int buf, int f0, int f1) { return halo_start(c, buf, f0, f1, false); }
+int pft_comm_halo_enqueue_comm(pft_comm* c, int buf, int f0, int f1) { return halo_start(c, buf, f0, f1, true); }
 
 int pft_comm_halo_finish(pft_comm* c)
 {
@@ -301,7 +310,10 @@ int pft_comm_eps_publish(pft_comm* c)
     NCCLCHK(ncclAllReduce(d, d, 2, ncclUint64, ncclMax, c->nccl, cs));
     return pft_slab_eps_mark_on(s, (void*)cs);
   }
-  const int rc = pft_comm_allreduce_eps(c);
+  // loopback: the host-side max reads the error norm through the compute stream, which must
+  // first take in the comm stream's boundary launch of stage 5
+  int rc = pft_slab_order(s, 1);
+  if (!rc) rc = pft_comm_allreduce_eps(c);
   return rc ? rc : pft_slab_eps_mark(s);
 }
 

@@ -1168,6 +1168,9 @@ struct pft_slab {
   unsigned long long* host_pub_dev;  // its device address
   hipStream_t stream, comm;
   hipStream_t side;      // error-norm read-back while the compute stream runs ahead
+  int launch_comm;       // 1: stage kernels go to the comm stream (the N > 1 boundary planes)
+  hipEvent_t ev_order[3];  // stream-order events: [0] compute -> comm, [1] comm -> compute,
+                           // [2] the last boundary launch on the comm stream
   hipEvent_t ev_eps;     // recorded on the compute stream after the error norm is final
   int eps_marked;
   int kz;                // planes per workgroup z-march; 0 = automatic (one full round, see auto_kz)
@@ -1239,6 +1242,9 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
 #endif
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&s->ev_eps, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&s->ev_order[0], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&s->ev_order[1], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&s->ev_order[2], hipEventDisableTiming);
   if (e == hipSuccess) e = hipMalloc((void**)&s->scratch, 64);
   if (e == hipSuccess) e = hipHostMalloc((void**)&s->host_scratch, 64, hipHostMallocDefault);
   if (e == hipSuccess) e = hipHostMalloc((void**)&s->host_pub, 64, hipHostMallocMapped | hipHostMallocCoherent);
@@ -1279,6 +1285,8 @@ int pft_slab_destroy(pft_slab* s)
   if (s->comm) (void)hipStreamDestroy(s->comm);
   if (s->side) (void)hipStreamDestroy(s->side);
   if (s->ev_eps) (void)hipEventDestroy(s->ev_eps);
+  for (int i = 0; i < 3; ++i)
+    if (s->ev_order[i]) (void)hipEventDestroy(s->ev_order[i]);
   delete s;
   return 0;
 }
@@ -1617,10 +1625,11 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   a.em1 = s->d.eps_mult[1];
   a.em2 = s->d.eps_mult[2];
   dim3 g((unsigned)(a.ntile * a.nchunk));
+  const hipStream_t st = s->launch_comm ? s->comm : s->stream;
   if (gls)
-    launch_stage<true>(stage, mode, kind, wx, g, s->stream, a, s->c);
+    launch_stage<true>(stage, mode, kind, wx, g, st, a, s->c);
   else
-    launch_stage<false>(stage, mode, kind, wx, g, s->stream, a, s->c);
+    launch_stage<false>(stage, mode, kind, wx, g, st, a, s->c);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1678,6 +1687,32 @@ int pft_slab_set_noise(pft_slab* s, const double* host_noise)
   const size_t bytes = sizeof(double) * (size_t)s->plane * s->d.n3;
   if (!s->noise) HIPCHK(hipMalloc((void**)&s->noise, bytes));
   HIPCHK(hipMemcpy(s->noise, host_noise, bytes, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int pft_slab_launch_on_comm(pft_slab* s, int on)
+{
+  s->launch_comm = on ? 1 : 0;
+  return 0;
+}
+
+int pft_slab_order(pft_slab* s, int comm_first)
+{
+  // the second stream waits for the work enqueued so far on the first
+  hipStream_t from = comm_first ? s->comm : s->stream, to = comm_first ? s->stream : s->comm;
+  hipEvent_t ev = s->ev_order[comm_first ? 1 : 0];
+  HIPCHK(hipEventRecord(ev, from));
+  HIPCHK(hipStreamWaitEvent(to, ev, 0));
+  return 0;
+}
+
+int pft_slab_boundary_event(pft_slab* s, int wait)
+{
+  if (wait) {
+    HIPCHK(hipStreamWaitEvent(s->stream, s->ev_order[2], 0));
+  } else {
+    HIPCHK(hipEventRecord(s->ev_order[2], s->comm));
+  }
   return 0;
 }
 

@@ -214,15 +214,27 @@ static int do_stage(int stage, double ts, double coef, double h, long * launches
 		if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
 		return rc;
 	}
-	/* both boundary planes first (one launch), their exchange overlaps the interior sweep
-	    */
+	/* Two streams.  Stage s reads the stage-(s-1) values of planes -1..n3 and writes
+	   its own; only its two boundary planes read ghost planes.  Compute stream: the interior
+	   sweep, once the previous stage's boundary planes (comm stream) are written -- not their
+	   exchange.  Comm stream: once the compute stream's previous interior sweep is done, the two
+	   boundary planes in one launch, then their exchange, beside this stage's interior sweep; the
+	   next stage's boundary launch follows the exchange in stream order. */
 	n3 = R.slab_grid.n3;
-	if((rc = run1(stage, ts, coef, h, PFT_K_BOUNDARY, 0))) return rc;
-	if((rc = pft_comm_halo_start(c, out_buf, 0, nfields))) return rc;
+	if((rc = pft_slab_order(R.slab, 0))) return rc;
+	if((rc = pft_slab_boundary_event(R.slab, 1))) return rc;
+	/* the boundary launch is enqueued first: both launches become ready when the previous
+	   interior sweep ends, and the comm stream's (greatest-priority) workgroups go first */
+	pft_slab_launch_on_comm(R.slab, 1);
+	rc = run1(stage, ts, coef, h, PFT_K_BOUNDARY, 0);
+	pft_slab_launch_on_comm(R.slab, 0);
+	if(rc) return rc;
+	if((rc = pft_slab_boundary_event(R.slab, 0))) return rc;
+	if((rc = pft_comm_halo_enqueue_comm(c, out_buf, 0, nfields))) return rc;
 	if(n3 > 2 && (rc = run1(stage, ts, coef, h, 1, n3-1))) return rc;
 	if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
 	*launches += 2;
-	return pft_comm_halo_finish(c);
+	return 0;
 }
 
 /* shared prologue results */
@@ -277,7 +289,11 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 			/* eps max over ranks (:572) and its publication beside the speculative stage 1 */
 			if((rc = pft_comm_eps_publish(c))) return rc;
 			if((rc = do_stage(6, t+h, 0.0, h, &launches))) return rc;
-		} else if((rc = pft_comm_allreduce_eps(c))) return rc;                  /* :572 */
+		} else {
+			/* the boundary launch of stage 5 (comm stream) adds to the error norm too */
+			if(pft_comm_splits(c) && (rc = pft_slab_order(R.slab, 1))) return rc;
+			if((rc = pft_comm_allreduce_eps(c))) return rc;                      /* :572 */
+		}
 		if((rc = pft_slab_eps_fetch(R.slab, &eps, &nonfinite))) return rc;
 		if(R.opt_timing) pft_slab_timing_collect(R.slab, R.stats.stage_ms, R.stats.stage_n);
 		system->steps_total++;                                                   /* :460 */
@@ -341,6 +357,8 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 		}
 	}
 	(void)rank;
+	/* join the comm stream (the last boundary launch and exchange) before the state leaves */
+	if(pft_comm_splits(c) && (rc = pft_slab_order(R.slab, 1))) return rc;
 	if(ret != 1 && ret != -4) system->t = t;                                     /* :768 */
 	if(R.opt_timing) pft_slab_timing_flush(R.slab, R.stats.stage_ms, R.stats.stage_n);
 	R.tstep = 0;
