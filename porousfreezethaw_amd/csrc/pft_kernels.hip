@@ -29,6 +29,11 @@
 #pragma clang fp contract(off)
 
 #define PFT_BLOCK 256
+// threads per workgroup of the fused stage kernel.  A/B: 512 (25 x 20-pair tiles, a third fewer
+// halo loads) measured 3-5% slower at 400^3 -- one workgroup per CU where 256 fit two to four
+#ifndef PFT_FBLOCK
+#define PFT_FBLOCK 256
+#endif
 #define PFT_TRING 8
 
 // recompute path: the gl components of K1..K4 are the literal zeros of dgl (equation.c:731,874),
@@ -56,11 +61,11 @@
 #define PFT_S5_FACE PFT_GLK_LITERAL
 #endif
 // stages with the two-deep z pipeline.  Measured at 400^3 (A/B, same box): faithful stages 3-4
-// 0.258 vs 0.288 / 0.296 ms once gl's K's became literals (operands as few as gl_static's); stage 1
-// no gain (its one input is x); stage 2 0.214-0.221 vs 0.228-0.230 before it carried K1 for the
-// K1 + K2 sum (PFT_K12_SUM), 0.250 vs 0.238 after (180 VGPRs: 2 waves)
+// 0.258 vs 0.288 / 0.296 ms once gl's K's became literals (operands as few as gl_static's); with
+// the tiles fitted to n1 (25 x 10 pairs) stage 1 0.158 vs 0.166 ms (148 VGPRs, 3 waves instead of
+// 4) and stage 2 0.217 vs 0.222 (182 VGPRs, 2 waves)
 #ifndef PFT_DEEP_MASK
-#define PFT_DEEP_MASK ((1 << 3) | (1 << 4))
+#define PFT_DEEP_MASK ((1 << 1) | (1 << 2) | (1 << 3) | (1 << 4))
 #endif
 #ifndef PFT_DEEP_ALL
 #define PFT_DEEP_ALL PFT_GLK_LITERAL
@@ -484,7 +489,11 @@ __global__ __launch_bounds__(PFT_BLOCK) void merson_stage(StageArgs a, pft_const
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
 // LDS doubles per field and plane of merson_fused: (2 gwx + 4)(gty + 2) <= 680 (64 x 8 tiles)
+#if PFT_FBLOCK > 256
+#define PFT_FUSED_LF 1224
+#else
 #define PFT_FUSED_LF 680
+#endif
 
 template <int WX>
 struct TileGeo {
@@ -756,7 +765,7 @@ __device__ __forceinline__ void keep5(int q, const Ops& r, dbl2& x, dbl2& k1, db
 }
 
 template <int STAGE, int MODE, bool GLS>
-__global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_S5_WAVES2 && STAGE == 5) || ((GLS || PFT_DEEP_ALL) && ((PFT_DEEP_MASK >> STAGE) & 1)) ? 2 : PFT_FUSED_WAVES))) void merson_fused(StageArgs a, pft_consts c)
+__global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT_S5_WAVES2 && STAGE == 5) || ((GLS || PFT_DEEP_ALL) && ((PFT_DEEP_MASK >> STAGE) & 1)) ? 2 : PFT_FUSED_WAVES))) void merson_fused(StageArgs a, pft_consts c)
 {
   // tile geometry chosen by the host per grid (fused_geometry): gwx pairs x gty rows, so that the
   // tiles fit n1 and n2 without mostly-idle edge workgroups (n1 = 200: 50 x 10 cells)
@@ -1010,8 +1019,8 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
   }
 
   if (STAGE == 5) {
-    __shared__ double red[PFT_BLOCK / 64];
-    __shared__ int rnf[PFT_BLOCK / 64];
+    __shared__ double red[PFT_FBLOCK / 64];
+    __shared__ int rnf[PFT_FBLOCK / 64];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
       const double ov = __shfl_xor(m, off, 64);
@@ -1027,7 +1036,7 @@ __global__ __launch_bounds__(PFT_BLOCK) __attribute__((amdgpu_waves_per_eu((PFT_
     if (threadIdx.x == 0) {
       double bm = red[0];
       int bnf = rnf[0];
-      for (int q = 1; q < PFT_BLOCK / 64; ++q) {
+      for (int q = 1; q < PFT_FBLOCK / 64; ++q) {
         if (red[q] > bm) bm = red[q];
         bnf |= rnf[q];
       }
@@ -1366,7 +1375,7 @@ static int kernel_occupancy(int kind, int wx)
                                             : (const void*)merson_tile<STAGE, MODE, GLS, 32>)
                                 : (const void*)merson_stage<STAGE, MODE, GLS>;
   int b = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, PFT_BLOCK, 0) != hipSuccess || b < 1) b = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, kind == KFUSED ? PFT_FBLOCK : PFT_BLOCK, 0) != hipSuccess || b < 1) b = 1;
   n = b;
   return n;
 }
@@ -1399,7 +1408,7 @@ template <int STAGE, int MODE, bool GLS>
 static void launch_kernel(int kind, int wx, dim3 g, hipStream_t st, const StageArgs& a, const pft_consts& c)
 {
   if (kind == KFUSED) {
-    merson_fused<STAGE, MODE, GLS><<<g, PFT_BLOCK, 0, st>>>(a, c);
+    merson_fused<STAGE, MODE, GLS><<<g, PFT_FBLOCK, 0, st>>>(a, c);
   } else if (kind == KTILE) {
     if (wx == 16)
       merson_tile<STAGE, MODE, GLS, 16><<<g, PFT_BLOCK, 0, st>>>(a, c);
@@ -1444,7 +1453,7 @@ extern "C" {
 // (2 wx + 4)(ty + 2) <= PFT_FUSED_LF doubles of LDS per field and plane.
 static bool fused_geometry_ok(int wx, int ty)
 {
-  return wx >= 4 && ty >= 1 && wx * ty <= PFT_BLOCK && 3 * (2 * wx + 4 + 2 * ty) <= PFT_BLOCK &&
+  return wx >= 4 && ty >= 1 && wx * ty <= PFT_FBLOCK && 3 * (2 * wx + 4 + 2 * ty) <= PFT_FBLOCK &&
          (2 * wx + 4) * (ty + 2) <= PFT_FUSED_LF;
 }
 
@@ -1460,10 +1469,10 @@ static double fused_geometry(int n1, int n2, int* wx_out, int* ty_out)
   double best = -1.0;
   int bw = 32, bt = 8;
   for (int wx = 16; wx <= 40; ++wx) {
-    int ty = PFT_BLOCK / wx;
+    int ty = PFT_FBLOCK / wx;
     while (ty > 1 && !fused_geometry_ok(wx, ty)) --ty;
     if (!fused_geometry_ok(wx, ty)) continue;
-    const long lanes = (long)((np + wx - 1) / wx) * ((n2 + ty - 1) / ty) * PFT_BLOCK;
+    const long lanes = (long)((np + wx - 1) / wx) * ((n2 + ty - 1) / ty) * PFT_FBLOCK;
     const double eff = (double)np * n2 / (double)lanes;
     if (eff >= best - 0.005) {
       if (eff > best) best = eff;
@@ -1512,7 +1521,7 @@ int pft_slab_tile_geometry(const pft_slab* s, int stage, int* wx, int* ty)
     fused_geometry(s->d.n1, s->d.n2, wx, ty);
   } else {
     *wx = auto_tile ? (stage <= 2 ? 16 : 32) : s->tile_wx;
-    *ty = PFT_BLOCK / *wx;
+    *ty = (kind == KFUSED ? PFT_FBLOCK : PFT_BLOCK) / *wx;
   }
   return kind;
 }
@@ -1573,7 +1582,7 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
       fused_geometry(s->d.n1, s->d.n2, &a.gwx, &a.gty);
     } else {
       a.gwx = s->tile_wx;
-      a.gty = PFT_BLOCK / s->tile_wx;
+      a.gty = PFT_FBLOCK / s->tile_wx;
     }
     if (!fused_geometry_ok(a.gwx, a.gty)) return -2;
     a.ntile = ((s->d.n1 + 2 * a.gwx - 1) / (2 * a.gwx)) * ((s->d.n2 + a.gty - 1) / a.gty);
