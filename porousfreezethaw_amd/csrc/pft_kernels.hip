@@ -1596,24 +1596,28 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   if (s->kz > 0) {
     a.kz = s->kz;
   } else {
-    // automatic: a CU runs `occ` workgroups at a time, so a chunk count costs
-    //   rounds x (kz + 2) = ceil(ceil(workgroups / CUs) / occ) x (planes per chunk + the two
-    // planes a chunk re-reads below and above); the cheapest count wins (more chunks only when 5% cheaper).
-    // Measured on a 400 x 400 x 100 slab (320 tiles; one 800^3 8-way rank), stages 4-5 at 2
-    // workgroups per CU: 3 chunks (960 workgroups, 2 rounds) 0.261 / 0.349 ms against 0.314 /
-    // 0.436 for the one-round choice (1 chunk: 64 CUs with 2 workgroups, 192 with 1); at 400^3
-    // (80 tiles) it keeps the one-round choices (stage 5: 6 chunks, 480 workgroups).
+    // automatic: a CU runs `occ` workgroups at a time; a chunk count with w = ceil(workgroups /
+    // CUs) workgroups per CU costs (planes per chunk + the two planes a chunk re-reads) times
+    //   - occ <= 2: ceil(w / occ) rounds -- a partial last round runs a CU at half its waves and
+    //     the HBM-bound stages stall;
+    //   - occ >= 3: max(1, w / occ) -- retiring workgroups are refilled at once, and the extra
+    //     workgroups help the arithmetic-heavy stages hide latency.
+    // The cheapest count wins (more chunks only when 5% cheaper).  Measured at 400^3 (80 tiles):
+    // stage 5 (occ 2) 6 chunks, 0.348 ms vs 0.393 for 16; stage 1 (occ 3) 16 chunks of 25 planes,
+    // 0.153 vs 0.163 for 9 of 45.  On a 400 x 400 x 100 slab (320 tiles, one 800^3 8-way rank)
+    // stages 4-5: 3 chunks (960 workgroups, 2 rounds) 0.261 / 0.349 ms against 0.314 / 0.436 for
+    // one round of 320 (64 CUs with 2 workgroups, 192 with 1).
     const int occ = stage_occupancy(stage, mode, gls, kind, wx);
     int best_nch = 1;
-    long best_cost = -1;
+    double best_cost = -1.0;
     for (int nch = 1; nch <= nplanes; ++nch) {
       const int kz = (nplanes + nch - 1) / nch;
       if (nch > 1 && kz == (nplanes + nch - 2) / (nch - 1)) continue;   // same kz as nch - 1
       const long nb = (long)a.ntile * ((nplanes + kz - 1) / kz);
       const long per_cu = (nb + s->n_cu - 1) / s->n_cu;
-      const long rounds = (per_cu + occ - 1) / occ;
-      const long cost = rounds * (kz + 2);
-      if (best_cost < 0 || 20 * cost < 19 * best_cost) { best_cost = cost; best_nch = nch; }
+      const double rounds = occ <= 2 ? (double)((per_cu + occ - 1) / occ) : std::max(1.0, (double)per_cu / occ);
+      const double cost = rounds * (kz + 2);
+      if (best_cost < 0.0 || cost < 0.95 * best_cost) { best_cost = cost; best_nch = nch; }
     }
     a.kz = (nplanes + best_nch - 1) / best_nch;
   }
