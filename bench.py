@@ -85,6 +85,9 @@ def parse():
                     help="diagnostic, 1 GPU: run the N>1 stage pipeline (boundary planes first, RCCL halo "
                          "exchange on the comm stream beside the interior sweep, RCCL eps max) with a "
                          "1-rank communicator exchanging with itself; never the headline value")
+    ap.add_argument("--two-stream", action="store_true",
+                    help="N>1 stage pipeline on two streams (boundary launch and exchange on the comm stream "
+                         "beside the interior sweep) instead of the default one-stream pipeline")
     ap.add_argument("--probe", type=int, default=0,
                     help="after the run, launch the 8-B/lane copy probe this many times "
                          "(rocprofv3 FETCH_SIZE/WRITE_SIZE calibration, known bytes)")
@@ -141,6 +144,7 @@ def main():
             assert L.pft_comm_set_self_exchange(comm, 1) == 0
             L.pft_comm_set_current(comm)
     L.pft_solver_set_option(P.PFT_OPT_DEVICE, dev)
+    L.pft_solver_set_option(P.PFT_OPT_ONE_STREAM, 0 if a.two_stream else 1)
 
     def barrier():
         if dist is not None:
@@ -243,6 +247,7 @@ def main():
                    "gl_static": a.gl_static, "kz": a.kz or "auto", "tile": a.tile, "recompute": not a.no_recompute,
                    "accepted_steps_total": int(sim.system.steps), "t_end": sim.t,
                    "host_boundary": a.host_boundary, "self_exchange": a.self_exchange,
+                   "pipeline": "two-stream" if a.two_stream else "one-stream",
                    "tiles": ({str(k): ("cache" if v[0] == 0 else f"{2 * v[1]}x{v[2]} cells")
                               for k, v in geo.items()} if geo else None)},
         "roofline": roof,

@@ -39,8 +39,12 @@ enum {
 	PFT_OPT_TILE = 5,       /* stage kernel: 1 (default) = automatic, 2 = LDS-tiled at any size with
 	                           the automatic tile, 32 / 16 = LDS-tiled 64x8 / 32x16 tiles, 0 =
 	                           cache-based kernel (pft_slab_set_tile) */
-	PFT_OPT_RECOMPUTE = 6   /* 1 (default): rebuild stage inputs from x and the K's inside the
+	PFT_OPT_RECOMPUTE = 6,  /* 1 (default): rebuild stage inputs from x and the K's inside the
 	                           stencil, 0: materialise the aux arrays (pft_slab_set_recompute) */
+	PFT_OPT_ONE_STREAM = 7  /* N > 1 stage pipeline: 1 (default) = one compute stream (boundary
+	                           launch, the exchange on the comm stream beside the interior sweep,
+	                           wait); 0 = two streams (boundary launch and exchange on the comm
+	                           stream beside the interior sweep) */
 };
 int pft_solver_set_option(int opt, long value);
 

@@ -40,12 +40,13 @@ typedef struct {
 	int *d_cs, *d_cz; double * d_cm; int d_nch, d_cap;
 	double *h_k, *h_aux; int h_cap;
 	/* options */
-	int opt_gls, opt_kz, opt_dev, opt_timing, opt_tile, opt_norecompute;
+	int opt_gls, opt_kz, opt_dev, opt_timing, opt_tile, opt_norecompute, opt_one_stream;
 	int tstep;                  /* this attempted step's stages are timed (every opt_timing-th) */
 	pft_solver_stats stats;
 } solver_state;
 
-static __thread solver_state R = { .slab_dev = -1, .opt_kz = 0, .opt_dev = -1, .opt_tile = 1 };
+static __thread solver_state R = { .slab_dev = -1, .opt_kz = 0, .opt_dev = -1, .opt_tile = 1,
+                                   .opt_one_stream = 1 };
 
 static pft_comm * comm(void)
 {
@@ -121,6 +122,7 @@ int pft_solver_set_option(int opt, long value)
 		case PFT_OPT_KZ: if(value < 0) return -2; R.opt_kz = (int)value; if(R.slab) pft_slab_set_kz(R.slab, R.opt_kz); return 0;
 		case PFT_OPT_DEVICE: R.opt_dev = (int)value; return 0;
 		case PFT_OPT_TIMING: if(value < 0) return -2; R.opt_timing = (int)value; return 0;
+		case PFT_OPT_ONE_STREAM: R.opt_one_stream = value ? 1 : 0; return 0;
 		case PFT_OPT_RECOMPUTE:
 			R.opt_norecompute = value ? 0 : 1; if(R.slab) pft_slab_set_recompute(R.slab, !R.opt_norecompute); return 0;
 		case PFT_OPT_TILE:
@@ -221,6 +223,16 @@ static int do_stage(int stage, double ts, double coef, double h, long * launches
 	   boundary planes in one launch, then their exchange, beside this stage's interior sweep; the
 	   next stage's boundary launch follows the exchange in stream order. */
 	n3 = R.slab_grid.n3;
+	if(R.opt_one_stream) {
+		/* one stream: both boundary planes, their exchange beside the interior sweep, then the
+		   compute stream waits for the exchange */
+		if((rc = run1(stage, ts, coef, h, PFT_K_BOUNDARY, 0))) return rc;
+		if((rc = pft_comm_halo_start(c, out_buf, 0, nfields))) return rc;
+		if(n3 > 2 && (rc = run1(stage, ts, coef, h, 1, n3-1))) return rc;
+		if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
+		*launches += 2;
+		return pft_comm_halo_finish(c);
+	}
 	if((rc = pft_slab_order(R.slab, 0))) return rc;
 	if((rc = pft_slab_boundary_event(R.slab, 1))) return rc;
 	/* the boundary launch is enqueued first: both launches become ready when the previous

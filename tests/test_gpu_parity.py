@@ -151,7 +151,7 @@ def test_matches_oracle_larger_grid(dims, flavour):
     sim.close()
 
 
-def _loopback_run(meta, initial, nprocs, times, mode=0, gl_static=False, flavour="fused32"):
+def _loopback_run(meta, initial, nprocs, times, mode=0, gl_static=False, flavour="fused32", one_stream=1):
     L = P.lib()
     group = C.c_void_p()
     assert L.pft_comm_init_loopback(C.byref(group), nprocs) == 0
@@ -162,6 +162,7 @@ def _loopback_run(meta, initial, nprocs, times, mode=0, gl_static=False, flavour
             mine = C.c_void_p()
             assert L.pft_comm_loopback_rank(group, r, C.byref(mine)) == 0
             L.pft_comm_set_current(mine)
+            L.pft_solver_set_option(P.PFT_OPT_ONE_STREAM, one_stream)   # per host thread
             Pm, info = O.params_from_meta(meta)
             sim = P.Simulation(info["n1"], info["n2"], info["n3"], (info["L1"], info["L2"], info["L3"]), mode,
                                Pm, nprocs=nprocs, rank=r, initial=initial, tau=1.0, tau_min=info["tau_min"],
@@ -189,15 +190,17 @@ def _loopback_run(meta, initial, nprocs, times, mode=0, gl_static=False, flavour
     return out
 
 
+@pytest.mark.parametrize("one_stream", [1, 0])
 @pytest.mark.parametrize("nprocs", [2, 4])
 @pytest.mark.parametrize("gl_static", [False, True])
 @pytest.mark.parametrize("flavour", ["default", "fused32", "tile16", "cache"])
-def test_multislab_loopback_bitwise(nprocs, gl_static, flavour):
+def test_multislab_loopback_bitwise(nprocs, gl_static, flavour, one_stream):
     """Z-slab decomposition with halo exchange (boundary planes first, interior overlapped) over
     the loopback transport on one GPU: identical to the single-slab reference trajectory (F6)"""
     meta, A = O.load_case("g20")
     times = meta["traj_times"][:2]
-    out = _loopback_run(meta, A["traj_m0_ic"], nprocs, times, gl_static=gl_static, flavour=flavour)
+    out = _loopback_run(meta, A["traj_m0_ic"], nprocs, times, gl_static=gl_static, flavour=flavour,
+                        one_stream=one_stream)
     for i in range(len(times)):
         ref = meta["traj_m0"][i]
         for r in range(nprocs):
@@ -218,9 +221,10 @@ def _self_exchange_comm():
     return comm
 
 
+@pytest.mark.parametrize("one_stream", [1, 0])
 @pytest.mark.parametrize("gl_static", [False, True])
 @pytest.mark.parametrize("flavour", ["default", "fusedauto", "fused16", "tile32", "cache"])
-def test_rccl_stage_pipeline_self_exchange_bitwise(gl_static, flavour):
+def test_rccl_stage_pipeline_self_exchange_bitwise(gl_static, flavour, one_stream):
     """the N > 1 stage pipeline through real RCCL calls on one GPU (pft_comm_set_self_exchange):
     both boundary planes in one launch, ncclSend/ncclRecv on the priority comm stream beside the
     interior sweep, the eps max by ncclAllReduce and its publication on the comm stream.  The
@@ -229,6 +233,7 @@ def test_rccl_stage_pipeline_self_exchange_bitwise(gl_static, flavour):
     L = P.lib()
     comm = _self_exchange_comm()
     L.pft_comm_set_current(comm)
+    L.pft_solver_set_option(P.PFT_OPT_ONE_STREAM, one_stream)
     try:
         meta, A = O.load_case("g20")
         sim, Pm, info = make_sim(meta, A["traj_m0_ic"], mode=0, gl_static=gl_static, flavour=flavour)
@@ -240,6 +245,7 @@ def test_rccl_stage_pipeline_self_exchange_bitwise(gl_static, flavour):
             assert np.array_equal(sim.interior(), A[f"traj_m0_state{i}"])
         sim.close()
     finally:
+        L.pft_solver_set_option(P.PFT_OPT_ONE_STREAM, 1)
         L.pft_comm_set_current(None)
         L.pft_comm_destroy(comm)
 
