@@ -88,6 +88,9 @@ def parse():
     ap.add_argument("--two-stream", action="store_true",
                     help="N>1 stage pipeline on two streams (boundary launch and exchange on the comm stream "
                          "beside the interior sweep) instead of the default one-stream pipeline")
+    ap.add_argument("--wave", type=int, default=0,
+                    help="W > 0: a step's five stages as a skewed z-wavefront of W-plane launches "
+                         "(PFT_OPT_WAVE; N = 1)")
     ap.add_argument("--probe", type=int, default=0,
                     help="after the run, launch the 8-B/lane copy probe this many times "
                          "(rocprofv3 FETCH_SIZE/WRITE_SIZE calibration, known bytes)")
@@ -145,6 +148,7 @@ def main():
             L.pft_comm_set_current(comm)
     L.pft_solver_set_option(P.PFT_OPT_DEVICE, dev)
     L.pft_solver_set_option(P.PFT_OPT_ONE_STREAM, 0 if a.two_stream else 1)
+    L.pft_solver_set_option(P.PFT_OPT_WAVE, a.wave)
 
     def barrier():
         if dist is not None:
@@ -194,8 +198,10 @@ def main():
     roof = None
     if not a.no_timing and stats.stage_n[1] > 0:
         per = {}
+        # wavefront (--wave): stages 2..5 are timed per launch, nl[s] launches of W planes per step
+        nl = wave_launches(sim.grid.n3, a.wave) if a.wave and world == 1 else {s: 1 for s in range(1, 6)}
         for s in range(1, 6):
-            ms = stats.stage_ms[s] / max(1, stats.stage_n[s])
+            ms = stats.stage_ms[s] / max(1, stats.stage_n[s]) * nl[s]     # per step
             byts = STAGE_DOUBLES[a.gl_static][s] * 8 * cells_rank
             per[s] = (ms, byts)
         dom = max(per, key=lambda s: per[s][0])
@@ -203,7 +209,7 @@ def main():
         achieved = byts / (ms * 1e-3) / 1e9
         traffic = None
         pmc = os.path.join(REPO, "profiles", "pmc_summary.json")
-        if os.path.exists(pmc):
+        if os.path.exists(pmc) and not a.wave:
             try:
                 ps = json.load(open(pmc))
                 key = f"stage{dom}_gl{int(a.gl_static)}_{n1}x{n2}x{sim.grid.n3}_m{a.mode}"
@@ -213,8 +219,8 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "kernel": kernel_name(dom, a, rc_path, n1),
-                "algorithmic_bytes_per_launch": byts,
-                "avg_launch_ms": round(ms, 4),
+                "algorithmic_bytes_per_launch": byts // nl[dom],
+                "avg_launch_ms": round(ms / nl[dom], 4),
                 "stages_ms": {str(s): round(per[s][0], 4) for s in per},
                 "stages_GBps": {str(s): round(per[s][1] / (per[s][0] * 1e-3) / 1e9, 1) for s in per}}
 
@@ -247,7 +253,7 @@ def main():
                    "gl_static": a.gl_static, "kz": a.kz or "auto", "tile": a.tile, "recompute": not a.no_recompute,
                    "accepted_steps_total": int(sim.system.steps), "t_end": sim.t,
                    "host_boundary": a.host_boundary, "self_exchange": a.self_exchange,
-                   "pipeline": "two-stream" if a.two_stream else "one-stream",
+                   "pipeline": "two-stream" if a.two_stream else "one-stream", "wave": a.wave,
                    "tiles": ({str(k): ("cache" if v[0] == 0 else f"{2 * v[1]}x{v[2]} cells")
                               for k, v in geo.items()} if geo else None)},
         "roofline": roof,
@@ -298,6 +304,16 @@ def workload(grid_nodes, world, shape="cube", literal_cube=False, mode=0, domain
     base = PR.default_params(grid_nodes=grid_nodes, calc_mode=mode, L=Lc)
     return (grid_nodes, base, (base["n1"], base["n2"], base["n3"] * world),
             (base["L1"], base["L2"], base["L3"] * world))
+
+
+def wave_launches(n3, w):
+    """launches per step of each stage in the wavefront schedule (rk_solver.c wave_stages);
+    stage 1 is the speculative launch, one per step"""
+    nl = {1: 1}
+    for s in range(2, 6):
+        nl[s] = sum(1 for c in range(0, (n3 + 4) // w + 2)
+                    if c * w - 4 < n3 and max(0, c * w - (s - 1)) < min(n3, (c + 1) * w - (s - 1)))
+    return nl
 
 
 def kernel_name(stage, a, rc_path, n1):

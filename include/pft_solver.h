@@ -30,8 +30,8 @@ int pft_solver_download(RK_MPI_S_SOLUTION * system);
 enum {
 	PFT_OPT_GL_STATIC = 1,  /* 1: exploit dgl == 0 (equation.c:731,874): gl neither stored in K
 	                           nor combined -- bit-identical results, less traffic. Default 0. */
-	PFT_OPT_KZ = 2,         /* planes per workgroup z-march; 0 (default) = automatic: one full
-	                           round of resident workgroups (pft_slab_set_kz) */
+	PFT_OPT_KZ = 2,         /* planes per workgroup z-march; 0 (default) = automatic: the z-chunk
+	                           cost model of pft_slab_set_kz */
 	PFT_OPT_DEVICE = 3,     /* HIP device of this thread's slab (default: current device) */
 	PFT_OPT_TIMING = 4,     /* N > 0: time the stages of every N-th attempted step with HIP events
 	                           (stats.stage_ms / stage_n); each timed stage adds ~3 us of
@@ -41,10 +41,14 @@ enum {
 	                           cache-based kernel (pft_slab_set_tile) */
 	PFT_OPT_RECOMPUTE = 6,  /* 1 (default): rebuild stage inputs from x and the K's inside the
 	                           stencil, 0: materialise the aux arrays (pft_slab_set_recompute) */
-	PFT_OPT_ONE_STREAM = 7  /* N > 1 stage pipeline: 1 (default) = one compute stream (boundary
+	PFT_OPT_ONE_STREAM = 7, /* N > 1 stage pipeline: 1 (default) = one compute stream (boundary
 	                           launch, the exchange on the comm stream beside the interior sweep,
 	                           wait); 0 = two streams (boundary launch and exchange on the comm
 	                           stream beside the interior sweep) */
+	PFT_OPT_WAVE = 8        /* one slab, fused path: W > 0 runs a step's five stages as a skewed
+	                           z-wavefront of W-plane launches (chunk c: stage s on planes
+	                           [cW - s + 1, (c+1)W - s + 1)), so each K is read back while it is
+	                           still in the Infinity Cache; 0 (default) = one launch per stage */
 };
 int pft_solver_set_option(int opt, long value);
 

@@ -29,6 +29,7 @@ RKA_CMD_FINISHED = 8
 PFT_SOLVE_KEEP_DEVICE, PFT_SOLVE_REUSE_DEVICE = 1, 2
 PFT_OPT_GL_STATIC, PFT_OPT_KZ, PFT_OPT_DEVICE, PFT_OPT_TIMING, PFT_OPT_TILE, PFT_OPT_RECOMPUTE = 1, 2, 3, 4, 5, 6
 PFT_OPT_ONE_STREAM = 7
+PFT_OPT_WAVE = 8
 MPI_COMM_WORLD = 0x44000000
 
 # every function of the public headers, for the "library exports its ABI" check

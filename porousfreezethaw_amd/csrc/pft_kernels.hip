@@ -813,15 +813,15 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT
   bool nf = false;
   dbl2 zm[3], zc[3], zp[3];
   constexpr bool FLUX = MODE != 10 && MODE != 11;
-  // face reuse (rhs_cell_f) in stages 1-4; stage 5 already holds ~250 VGPRs of combine operands
-  // and the z-face carry spills there (measured 0.505 vs 0.470 ms) -- except with gl_static,
-  // whose fewer operands leave room (0.389 vs 0.415 ms)
+  // face reuse (rhs_cell_f) in every stage.  Stage 5 holds two planes of combine operands; only
+  // with gl's K's literal (PFT_S5_FACE) or gl_static does the z-face carry fit beside them (235
+  // VGPRs, no spills; with gl's K's materialised it spilled: 0.505 vs 0.470 ms)
   constexpr bool FACE = STAGE != 5 || GLS || PFT_S5_FACE;
-  // two-deep z pipeline (stages in PFT_DEEP_MASK, gl_static builds): the raw operands of plane k+2
-  // are loaded while plane k is computed (the stage input of plane k+1 is its z+1 neighbour, so a
-  // one-deep pipeline waits for its loads before the stencil).  It costs the operand registers:
-  // 198 VGPRs = 2 waves/SIMD for stages 3-4.  Measured at 400^3: gl_static stages 3-4 0.275 vs
-  // 0.294 ms; faithful (3 evolving fields, more operands) 0.376 vs 0.370 -- kept off there.
+  // two-deep z pipeline (stages in PFT_DEEP_MASK; gl_static, and every mode once gl's K's are
+  // literal, PFT_DEEP_ALL): the raw operands of plane k+2 are loaded while plane k is computed (the
+  // stage input of plane k+1 is its z+1 neighbour, so a one-deep pipeline waits for its loads
+  // before the stencil).  It costs the operand registers: 2 waves/SIMD.  Measured at 400^3:
+  // stages 3-4 0.258 vs 0.288-0.296 ms, stage 1 0.158 vs 0.166, stage 2 0.217 vs 0.222.
   constexpr bool DEEP = (GLS || PFT_DEEP_ALL) && ((PFT_DEEP_MASK >> STAGE) & 1) != 0 && STAGE >= 1 && STAGE <= 4;
   Ops pn[3], ph;                       // DEEP: operands of plane k+1 (centre, halo pair)
   FaceT fz[2];                         // z-face below plane k of each cell of the pair
@@ -1182,7 +1182,7 @@ struct pft_slab {
                            // [2] the last boundary launch on the comm stream
   hipEvent_t ev_eps;     // recorded on the compute stream after the error norm is final
   int eps_marked;
-  int kz;                // planes per workgroup z-march; 0 = automatic (one full round, see auto_kz)
+  int kz;                // planes per workgroup z-march; 0 = automatic (z-chunk cost model)
   int n_cu;               // compute units of the slab's device
   double* noise;         // device u_noise (n3*plane) or null
   int tile_wx;           // 32 / 16: LDS-tiled kernels with that many pairs per row; 1: automatic;

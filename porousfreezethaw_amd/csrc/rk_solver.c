@@ -40,7 +40,7 @@ typedef struct {
 	int *d_cs, *d_cz; double * d_cm; int d_nch, d_cap;
 	double *h_k, *h_aux; int h_cap;
 	/* options */
-	int opt_gls, opt_kz, opt_dev, opt_timing, opt_tile, opt_norecompute, opt_one_stream;
+	int opt_gls, opt_kz, opt_dev, opt_timing, opt_tile, opt_norecompute, opt_one_stream, opt_wave;
 	int tstep;                  /* this attempted step's stages are timed (every opt_timing-th) */
 	pft_solver_stats stats;
 } solver_state;
@@ -123,6 +123,7 @@ int pft_solver_set_option(int opt, long value)
 		case PFT_OPT_DEVICE: R.opt_dev = (int)value; return 0;
 		case PFT_OPT_TIMING: if(value < 0) return -2; R.opt_timing = (int)value; return 0;
 		case PFT_OPT_ONE_STREAM: R.opt_one_stream = value ? 1 : 0; return 0;
+		case PFT_OPT_WAVE: if(value < 0) return -2; R.opt_wave = (int)value; return 0;
 		case PFT_OPT_RECOMPUTE:
 			R.opt_norecompute = value ? 0 : 1; if(R.slab) pft_slab_set_recompute(R.slab, !R.opt_norecompute); return 0;
 		case PFT_OPT_TILE:
@@ -216,12 +217,13 @@ static int do_stage(int stage, double ts, double coef, double h, long * launches
 		if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
 		return rc;
 	}
-	/* Two streams.  Stage s reads the stage-(s-1) values of planes -1..n3 and writes
-	   its own; only its two boundary planes read ghost planes.  Compute stream: the interior
-	   sweep, once the previous stage's boundary planes (comm stream) are written -- not their
-	   exchange.  Comm stream: once the compute stream's previous interior sweep is done, the two
-	   boundary planes in one launch, then their exchange, beside this stage's interior sweep; the
-	   next stage's boundary launch follows the exchange in stream order. */
+	/* SURVEY 8e.  Stage s reads the stage-(s-1) values of planes -1..n3 and writes its own; only
+	   its two boundary planes read ghost planes, so they are launched first and exchanged beside
+	   the interior sweep.  Default (one stream): boundary launch, the exchange on the comm stream
+	   beside the interior sweep, then the compute stream waits for the exchange.  Two streams
+	   (PFT_OPT_ONE_STREAM 0): the boundary launch and its exchange on the comm stream once the
+	   previous interior sweep is done; the interior sweep waits only for the previous stage's
+	   boundary launch. */
 	n3 = R.slab_grid.n3;
 	if(R.opt_one_stream) {
 		/* one stream: both boundary planes, their exchange beside the interior sweep, then the
@@ -246,6 +248,35 @@ static int do_stage(int stage, double ts, double coef, double h, long * launches
 	if(n3 > 2 && (rc = run1(stage, ts, coef, h, 1, n3-1))) return rc;
 	if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
 	*launches += 2;
+	return 0;
+}
+
+/* PFT_OPT_WAVE = W > 0 (one slab, fused path): the five stages of a step as a skewed z-wavefront
+   of W-plane launches.  Chunk c runs stage s on planes [cW - (s-1), (c+1)W - (s-1)), so every
+   plane a stage reads from the stage before it (its z+1 neighbour included) was written by an
+   earlier launch, and the K a stage writes is read back one launch later, while it is still in
+   the 256 MB Infinity Cache.  Each buffer is written by one stage only (K1, A0 = K1 + K2, K3, K4,
+   XN), so no launch overwrites what a later launch of the step reads.  Same kernels, same
+   arithmetic per cell: bit-identical to one launch per stage. */
+static int wave_stages(int do1, double t, double h, double h2, double h3, double h6, double h8,
+                       long * launches)
+{
+	const double ts[6] = {0.0, t, t+h3, t+h3, t+h2, t+h};
+	const double cf[6] = {0.0, h3, h6, h8, h, h3};
+	const int n3 = R.slab_grid.n3, W = R.opt_wave;
+	int c, s, rc;
+	for(c = 0; c*W - 4 < n3; c++)
+		for(s = do1 ? 1 : 2; s <= 5; s++) {
+			const int kb = c*W - (s-1) < 0 ? 0 : c*W - (s-1);
+			const int ke = (c+1)*W - (s-1) > n3 ? n3 : (c+1)*W - (s-1);
+			if(kb >= ke) continue;
+			(*launches)++;
+			/* sampled timing: every launch of stages 2..5 (stage 1 is timed on the speculative
+			   launch, one per step) */
+			if(R.tstep && s > 1) pft_slab_timing_mark(R.slab, s, 0);
+			if((rc = pft_slab_stage(R.slab, s, ts[s], cf[s], h, kb, ke))) return rc;
+			if(R.tstep && s > 1) pft_slab_timing_mark(R.slab, s, 1);
+		}
 	return 0;
 }
 
@@ -291,12 +322,17 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 		/* the error norm accumulator is reset by its publication on the speculative path */
 		if((!spec || attempted == 0) && (rc = pft_slab_eps_reset(R.slab))) return rc;
 		/* K1 = f(t,x); aux = x + K1 h/3 ... K5 = f(t+h, aux); error norm; x(t+h) candidate */
-		if(!(spec && k1_valid) && (rc = do_stage(1, t, h3, h, &launches))) return rc;  /* :373-389 */
+		if(R.opt_wave > 0 && spec && !pft_comm_splits(c)) {
+			/* the same five stages as a skewed z-wavefront of W-plane launches (wave_stages) */
+			if((rc = wave_stages(!k1_valid, t, h, h2, h3, h6, h8, &launches))) return rc;
+		} else {
+			if(!(spec && k1_valid) && (rc = do_stage(1, t, h3, h, &launches))) return rc;  /* :373-389 */
+			if((rc = do_stage(2, t+h3, h6, h, &launches))) return rc;    /* :392-409 */
+			if((rc = do_stage(3, t+h3, h8, h, &launches))) return rc;    /* :412-429 */
+			if((rc = do_stage(4, t+h2, h,  h, &launches))) return rc;    /* :432-450 */
+			if((rc = do_stage(5, t+h,  h3, h, &launches))) return rc;    /* :453,507-524,657-668 */
+		}
 		k1_valid = 1;
-		if((rc = do_stage(2, t+h3, h6, h, &launches))) return rc;    /* :392-409 */
-		if((rc = do_stage(3, t+h3, h8, h, &launches))) return rc;    /* :412-429 */
-		if((rc = do_stage(4, t+h2, h,  h, &launches))) return rc;    /* :432-450 */
-		if((rc = do_stage(5, t+h,  h3, h, &launches))) return rc;    /* :453,507-524,657-668 */
 		if(spec) {
 			/* eps max over ranks (:572) and its publication beside the speculative stage 1 */
 			if((rc = pft_comm_eps_publish(c))) return rc;

@@ -453,3 +453,76 @@ def test_rhs_with_temperature_noise(mode, flavour):
     dwo = np.zeros_like(w)
     O.lib().pft_or_stencil(C.byref(g), O.ptr(Pm), mode, O.ptr(w), O.ptr(noise), O.ptr(dwo))
     assert np.array_equal(K, O.unpad(g, dwo))
+
+
+@pytest.mark.parametrize("wave", [1, 3, 7])
+@pytest.mark.parametrize("gl_static", [False, True])
+@pytest.mark.parametrize("flavour", ["default", "fusedauto", "fused16", "fused32", "cache"])
+def test_wavefront_schedule_bitwise(wave, gl_static, flavour):
+    """PFT_OPT_WAVE (rk_solver.c wave_stages): a step's five stages as a skewed z-wavefront of
+    W-plane launches reach the reference trajectory bit for bit.  The cache kernel has no
+    recompute path and keeps one launch per stage; so does "default" here, which picks the cache
+    kernel for the 10-cell-wide g20 plane"""
+    L = P.lib()
+    assert L.pft_solver_set_option(P.PFT_OPT_WAVE, wave) == 0
+    try:
+        meta, A = O.load_case("g20")
+        sim, Pm, info = make_sim(meta, A["traj_m0_ic"], mode=0, gl_static=gl_static, flavour=flavour)
+        for i, T in enumerate(meta["traj_times"][:2]):
+            rc = sim.solve(T)
+            ref = meta["traj_m0"][i]
+            assert (sim.t.hex(), sim.h.hex(), sim.system.steps, sim.system.steps_total, rc) == \
+                (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(), ref[2], ref[3], ref[4])
+            assert np.array_equal(sim.interior(), A[f"traj_m0_state{i}"])
+        st = sim.stats()
+        if flavour not in ("cache", "default"):
+            assert st.kernel_launches > 6 * st.steps_total
+        else:
+            assert st.kernel_launches == 5 * st.steps_total
+        sim.close()
+    finally:
+        L.pft_solver_set_option(P.PFT_OPT_WAVE, 0)
+
+
+def test_wavefront_schedule_larger_grid():
+    """the wavefront on a 100 x 36 x 40 grid (W = 6: clipped first and last chunks, several
+    z-chunks per launch) vs the oracle, 12 attempted steps"""
+    L = P.lib()
+    assert L.pft_solver_set_option(P.PFT_OPT_WAVE, 6) == 0
+    try:
+        meta, A = O.load_case("g20")
+        Pm, info = O.params_from_meta(meta)
+        n1, n2, n3 = 100, 36, 40
+        info = dict(info, n1=n1, n2=n2, n3=n3)
+        sim = P.Simulation(n1, n2, n3, (info["L1"], info["L2"], info["L3"]), 0, Pm, beads=O.beads(), tau=1.0,
+                           tau_min=info["tau_min"], delta=info["delta"], tile=2)
+        ic = sim.interior()
+        assert sim.solve_ex(1e9, 12, 0) == 2
+        res = O.solve(info, Pm, 0, ic, 0.0, 1.0, [1e9], max_steps_total=12)[0]
+        assert (sim.t, sim.h, sim.system.steps, sim.system.steps_total) == (res[0], res[1], res[2], res[3])
+        assert np.array_equal(sim.interior(), res[5])
+        sim.close()
+    finally:
+        L.pft_solver_set_option(P.PFT_OPT_WAVE, 0)
+
+
+def test_full_size_400_wavefront_bitwise():
+    """400^3 at full size: 3 attempted steps as a skewed z-wavefront of 24-plane launches equal the
+    one-launch-per-stage run bit for bit"""
+    base, Pm, info = _full_size_case()
+    L3s = (info["L1"], info["L2"], info["L3"])
+    L = P.lib()
+    outs = []
+    for wave in (0, 24):
+        assert L.pft_solver_set_option(P.PFT_OPT_WAVE, wave) == 0
+        try:
+            s = P.Simulation(info["n1"], info["n2"], info["n3"], L3s, 0, Pm, beads=O.beads(), tau=1.0,
+                             tau_min=info["tau_min"], delta=info["delta"])
+            assert s.solve_ex(1e9, 3, 0) == 2
+            outs.append(((s.t, s.h, s.system.steps, s.system.steps_total), s.interior(), s.stats().kernel_launches))
+            s.close()
+        finally:
+            L.pft_solver_set_option(P.PFT_OPT_WAVE, 0)
+    assert outs[0][0] == outs[1][0]
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert outs[1][2] > outs[0][2]
