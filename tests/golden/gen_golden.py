@@ -17,7 +17,13 @@ Cases (SURVEY.md section 4.2 KATs 1-4):
            RHS for all modes on 1 and 4 ranks (ranks hold 8/8/7/7 planes), plus every
            rank's padded input array after bcond_setup+sync_solution (boundary KAT),
            and single-step solves (accepted and rejected-first).
+  g100     BASELINE configs[0]: default Params at grid_nodes 100 (50x50x100): parameters, the
+           SHA-256 of the IC and of a mode-0 trajectory to two snapshot times (checked identical
+           on 2 ranks), plus the middle and top z-planes of each state (a state is 6 MB).
+
+    python tests/golden/gen_golden.py [case ...]     (default: all)
 """
+import hashlib
 import json
 import os
 import re
@@ -157,6 +163,41 @@ def case_g20():
     return arrays, meta
 
 
+def sha256(a):
+    return hashlib.sha256(np.ascontiguousarray(a, dtype="<f8").tobytes()).hexdigest()
+
+
+G100_TIMES = [3.0, 10.0]
+
+
+def case_g100():
+    arrays, meta = {}, {"case": "g100", "source": "reference Params, grid_nodes 100"}
+    w = Work({"grid_nodes": 100})
+    try:
+        out = w.run(1, "setup")
+        p = read_params(out)
+        shape = (3, p["n3"], p["n2"], p["n1"])
+        ic = load(os.path.join(out, "ic.f64"), shape)
+        meta["params"] = hexify(p)
+        meta["ic_sha256"] = sha256(ic)
+        icp = os.path.join(w.dir, "ic.f64")
+        ic.tofile(icp)
+        o = w.run(1, "solve", icp, 0.0, 1.0, *G100_TIMES)
+        tm, st = traj(o, len(G100_TIMES), shape)
+        o2 = w.run(2, "solve", icp, 0.0, 1.0, *G100_TIMES)
+        tm2, st2 = traj(o2, len(G100_TIMES), shape)
+        assert tm == tm2 and all(np.array_equal(a, b) for a, b in zip(st, st2)), "decomposition invariance"
+        meta["traj_times"] = G100_TIMES
+        meta["traj_m0"] = tm
+        meta["traj_m0_sha256"] = [sha256(x) for x in st]
+        for i, x in enumerate(st):
+            arrays[f"traj_m0_state{i}_mid"] = x[:, shape[1] // 2]
+            arrays[f"traj_m0_state{i}_top"] = x[:, -1]
+    finally:
+        w.close()
+    return arrays, meta
+
+
 def case_ragged():
     arrays, meta = {}, {"case": "ragged", "source": "reference Params, L1=0.036 L2=0.024 grid_nodes 30"}
     rep = {"L1": 0.036, "L2": 0.024, "grid_nodes": 30}
@@ -206,8 +247,9 @@ def case_ragged():
 def main():
     if not os.path.exists(PFT_REF):
         sys.exit("build the reference harness first: make -C oracle ref")
-    for fn in (case_g20, case_ragged):
-        arrays, meta = fn()
+    cases = {"g20": case_g20, "ragged": case_ragged, "g100": case_g100}
+    for name in sys.argv[1:] or list(cases):
+        arrays, meta = cases[name]()
         name = meta["case"]
         np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrays)
         with open(os.path.join(HERE, f"{name}.json"), "w") as f:
