@@ -47,7 +47,8 @@ STAGE_DOUBLES_AUX = {False: {1: 9, 2: 12, 3: 15, 4: 18, 5: 18}, True: {1: 7, 2: 
 # recompute path: stage s reads the arrays its input is built from, writes K_s (stage 5: x(t+h));
 # gl's K's are the literal zeros of dgl (PFT_GLK_LITERAL, never stored or loaded), so a stage
 # reads x of all 3 fields, the K's of u and p, and writes K_s of u and p (stage 5: all of x(t+h));
-# stage 2 stores S = K1 + K2, so stage 3 reads x and S (PFT_K12_SUM)
+# stage 2 stores S = K1 + K2, so stage 3 reads x and S (PFT_K12_SUM); stage 5 stores gl's x(t+h)
+# only when it is not x itself (pft_slab_get_gl_keep: 11 doubles then, as with gl_static)
 STAGE_DOUBLES_RC = {False: {1: 5, 2: 7, 3: 7, 4: 9, 5: 12}, True: {1: 5, 2: 7, 3: 7, 4: 9, 5: 11}}
 SURVEY_BYTES_PER_CELL_STEP = 840   # unfused solver/RHS boundary accounting
 METRIC = "Mcells·RK-steps/s at 400³ grid, 1/2/4/8 MI355X; % HBM roofline"
@@ -193,6 +194,12 @@ def main():
         el = float(tt.item())
     stats = sim.stats()
     geo = sim.tile_geometry()
+    L.pft_slab_get_gl_keep.argtypes = [C.c_void_p]
+    L.pft_solver_slab.restype = C.c_void_p
+    gl_keep = bool(rc_path and L.pft_slab_get_gl_keep(L.pft_solver_slab()))
+    if gl_keep and not a.gl_static:
+        STAGE_DOUBLES = {g: dict(v) for g, v in STAGE_DOUBLES.items()}
+        STAGE_DOUBLES[False][5] = 11
 
     # ---- roofline: dominant fused stage kernel, HIP events on the slab's compute stream -----
     roof = None
@@ -254,6 +261,7 @@ def main():
                    "accepted_steps_total": int(sim.system.steps), "t_end": sim.t,
                    "host_boundary": a.host_boundary, "self_exchange": a.self_exchange,
                    "pipeline": "two-stream" if a.two_stream else "one-stream", "wave": a.wave,
+                   "gl_store_skipped": gl_keep,
                    "tiles": ({str(k): ("cache" if v[0] == 0 else f"{2 * v[1]}x{v[2]} cells")
                               for k, v in geo.items()} if geo else None)},
         "roofline": roof,

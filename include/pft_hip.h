@@ -89,6 +89,10 @@ int pft_slab_tile_geometry(const pft_slab * s, int stage, int * wx, int * ty);
    stencil (no aux arrays: 54 instead of 72 doubles of traffic per cell-step, bit-identical);
    0: the reference's aux arrays are materialised between stages */
 int pft_slab_set_recompute(pft_slab * s, int on);
+/* 1: X and XN hold the same gl field and no gl value is -0.0 or NaN (the caller checked), so
+   stage 5 need not store gl's x(t+h) = x + coef*0.0 (== x); cleared by every upload */
+int pft_slab_set_gl_keep(pft_slab * s, int on);
+int pft_slab_get_gl_keep(const pft_slab * s);   /* 1: stage 5 skips that store */
 /* buffer written by stage 1..5 of the step on this slab's path (its boundary planes are what
    the z-neighbours need before the next stage) */
 int pft_slab_stage_output(const pft_slab * s, int stage);

@@ -64,6 +64,10 @@
 // 0.258 vs 0.288 / 0.296 ms once gl's K's became literals (operands as few as gl_static's); with
 // the tiles fitted to n1 (25 x 10 pairs) stage 1 0.158 vs 0.166 ms (148 VGPRs, 3 waves instead of
 // 4) and stage 2 0.217 vs 0.222 (182 VGPRs, 2 waves)
+// stage 5 skips storing gl's x(t+h) when XN already holds it (pft_slab_set_gl_keep); 0 = always store
+#ifndef PFT_GL_KEEP
+#define PFT_GL_KEEP 1
+#endif
 #ifndef PFT_DEEP_MASK
 #define PFT_DEEP_MASK ((1 << 1) | (1 << 2) | (1 << 3) | (1 << 4))
 #endif
@@ -284,6 +288,7 @@ struct StageArgs {
   const double* k2;    // K2 (stored only on this path; the reference aliases it with K3)
   double cin;          // coefficient of the stage-input combine: h3, h6, h8, h for stages 2..5
   int gwx, gty;        // merson_fused tile: gwx cell pairs x gty rows (fused_geometry)
+  int gl_keep;         // stage 5: x(t+h) of gl is not stored, XN already holds it (pft_slab_set_gl_keep)
 };
 
 __device__ __forceinline__ int xcd_remap(int b, int n)
@@ -1001,7 +1006,7 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT
             nf |= !isfinite(ev);
             r[s] = ox[s] + a.coef * (0.5 * (ok1[s] + K[s]) + 2.0 * ok4[s]);                  // :667
           }
-          st2(a.out + e, r);
+          if (!(q == 2 && a.gl_keep)) st2(a.out + e, r);
         }
       }
     }
@@ -1189,6 +1194,7 @@ struct pft_slab {
                          // 2: LDS-tiled at any size, automatic tile; 0: cache-based
   int n1_tiled_ok;
   int recompute;         // 1: stage inputs rebuilt from x and the K's (no aux arrays)
+  int gl_keep;           // X and XN hold the same gl, and x + c*0.0 == x for every gl value
   // per-stage timing: a ring of begin/end event pairs, so that kernels still running when the
   // host collects (the speculative stage 1) are picked up by a later collect
   hipEvent_t tev[6][PFT_TRING][2];
@@ -1332,6 +1338,7 @@ static int ensure_staging(pft_slab* s)
 
 int pft_slab_upload_host(pft_slab* s, int which, const double* host_padded)
 {
+  s->gl_keep = 0;        // X and XN may differ now: the caller re-establishes it
   int rc = ensure_staging(s);
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(s->staging, host_padded, sizeof(double) * 3 * (size_t)s->S, hipMemcpyHostToDevice,
@@ -1634,6 +1641,10 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   // stage-input coefficients of the recompute path: exactly the solver's h/3.0, h/6.0, h/8.0, h
   a.cin = stage == 2 ? h / 3.0 : stage == 3 ? h / 6.0 : stage == 4 ? h / 8.0 : h;
   if (kind == KFUSED && in) a.x = in;    // pure RHS / speculative stage 1: the input is the given buffer
+  // gl's x(t+h) is x + coef*(0.5*(0.0 + 0.0) + 2.0*0.0) (gl's K's are literal zeros): equal to x
+  // bit for bit when coef is finite and no gl value is -0.0 or NaN, which the solver checked at
+  // upload (pft_slab_set_gl_keep); XN's gl then already holds it, and stage 5 skips that store
+  a.gl_keep = PFT_GL_KEEP && stage == 5 && kind == KFUSED && out && s->gl_keep && PFT_GLK_LITERAL && std::isfinite(coef) ? 1 : 0;
   a.em0 = s->d.eps_mult[0];
   a.em1 = s->d.eps_mult[1];
   a.em2 = s->d.eps_mult[2];
@@ -1671,6 +1682,14 @@ int pft_slab_rhs(pft_slab* s, int in_buf, int out_buf, double t)
   if (in_buf < 0 || in_buf >= PFT_BUF_COUNT || out_buf < 0 || out_buf >= PFT_BUF_COUNT) return -2;
   return run_stage(s, 0, s->buf[in_buf], s->buf[out_buf], nullptr, t, 0.0, 0.0, -1, -1, 0, slab_kind(s));
 }
+
+int pft_slab_set_gl_keep(pft_slab* s, int on)
+{
+  s->gl_keep = on ? 1 : 0;
+  return 0;
+}
+
+int pft_slab_get_gl_keep(const pft_slab* s) { return PFT_GL_KEEP && PFT_GLK_LITERAL && s->gl_keep; }
 
 int pft_slab_set_recompute(pft_slab* s, int on)
 {

@@ -280,6 +280,28 @@ static int wave_stages(int do1, double t, double h, double h2, double h3, double
 	return 0;
 }
 
+/* gl evolves by dgl == 0 (equation.c:731,874), so x(t+h) of gl is x + coef*0.0: x itself, bit for
+   bit, unless x is -0.0 (-0.0 + 0.0 = +0.0) or NaN.  When no gl value of the uploaded state is
+   either, X and XN (both uploaded from it) keep identical gl for good and stage 5 skips that store
+   (pft_slab_set_gl_keep); one step turns any -0.0 into +0.0, so the check only looks at input. */
+static int gl_clean(const double * x)
+{
+	/* host layout: [q][k][j][i] with 2 ghost cells on every side; only the interior is uploaded */
+	const int n1 = R.slab_grid.n1, n2 = R.slab_grid.n2, n3 = R.slab_grid.n3;
+	const long N1 = n1 + 4, N2 = n2 + 4;
+	const double * g = x + 2 * N1 * N2 * (n3 + 4);
+	int k, bad = 0;
+	#pragma omp parallel for reduction(|:bad) schedule(static)
+	for(k = 2; k < n3 + 2; k++) {
+		int j, i;
+		for(j = 2; j < n2 + 2; j++) {
+			const double * r = g + ((long)k * N2 + j) * N1;
+			for(i = 2; i < n1 + 2; i++) bad |= (r[i] != r[i]) || (r[i] == 0.0 && signbit(r[i]));
+		}
+	}
+	return !bad;
+}
+
 /* shared prologue results */
 typedef struct {
 	double final_time, t, h, h_min, delta;
@@ -302,6 +324,7 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	if(!(flags & PFT_SOLVE_REUSE_DEVICE) || !R.device_valid) {
 		if((rc = pft_slab_upload_host(R.slab, PFT_BUF_X, system->x))) return rc;
 		if((rc = pft_slab_upload_host(R.slab, PFT_BUF_XN, system->x))) return rc;
+		pft_slab_set_gl_keep(R.slab, gl_clean(system->x));
 		if(nprocs > 1) {
 			if((rc = pft_comm_halo(c, PFT_BUF_X, 0, 3))) return rc;
 			if((rc = pft_comm_halo(c, PFT_BUF_XN, 0, 3))) return rc;

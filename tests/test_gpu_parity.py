@@ -526,3 +526,31 @@ def test_full_size_400_wavefront_bitwise():
     assert outs[0][0] == outs[1][0]
     assert np.array_equal(outs[0][1], outs[1][1])
     assert outs[1][2] > outs[0][2]
+
+
+@pytest.mark.parametrize("flavour", ["default", "fusedauto"])
+def test_gl_negative_zero_keeps_reference_bits(flavour):
+    """stage 5 skips storing gl's x(t+h) = x + coef*0.0 when that is x bit for bit
+    (pft_slab_set_gl_keep); a -0.0 in gl (-0.0 + 0.0 = +0.0) must turn that off: 12 attempted
+    steps from a state with -0.0 and +0.0 in gl equal the oracle's bit for bit"""
+    meta, A = O.load_case("g20")
+    Pm, info = O.params_from_meta(meta)
+    n1, n2, n3 = 30, 30, 24
+    info = dict(info, n1=n1, n2=n2, n3=n3)
+    sim = P.Simulation(n1, n2, n3, (info["L1"], info["L2"], info["L3"]), 0, Pm, beads=O.beads(), tau=1.0,
+                       tau_min=info["tau_min"], delta=info["delta"], init_solver=False)
+    ic = sim.interior().copy()
+    sim.close()
+    ic[2, :, :5, :] = 0.0
+    ic[2, 3:9, :3, 2:11] = -0.0
+    assert np.signbit(ic[2]).sum() > 0
+    sim = P.Simulation(n1, n2, n3, (info["L1"], info["L2"], info["L3"]), 0, Pm, initial=ic, tau=1.0,
+                       tau_min=info["tau_min"], delta=info["delta"], tile=FLAVOURS[flavour][0],
+                       recompute=FLAVOURS[flavour][1])
+    assert sim.solve_ex(1e9, 12, 0) == 2
+    res = O.solve(info, Pm, 0, ic, 0.0, 1.0, [1e9], max_steps_total=12)[0]
+    assert (sim.t, sim.h, sim.system.steps, sim.system.steps_total) == (res[0], res[1], res[2], res[3])
+    got = sim.interior()
+    assert np.array_equal(got, res[5])
+    assert np.array_equal(np.signbit(got[2]), np.signbit(res[5][2]))
+    sim.close()
