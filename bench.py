@@ -89,6 +89,9 @@ def parse():
     ap.add_argument("--two-stream", action="store_true",
                     help="N>1 stage pipeline on two streams (boundary launch and exchange on the comm stream "
                          "beside the interior sweep) instead of the default one-stream pipeline")
+    ap.add_argument("--comm-boundary", action="store_true",
+                    help="N>1 stage pipeline: boundary launch and exchange on the comm stream, the interior "
+                         "sweep waiting for the boundary launch (PFT_OPT_ONE_STREAM 2)")
     ap.add_argument("--wave", type=int, default=0,
                     help="W > 0: a step's five stages as a skewed z-wavefront of W-plane launches "
                          "(PFT_OPT_WAVE; N = 1)")
@@ -148,7 +151,7 @@ def main():
             assert L.pft_comm_set_self_exchange(comm, 1) == 0
             L.pft_comm_set_current(comm)
     L.pft_solver_set_option(P.PFT_OPT_DEVICE, dev)
-    L.pft_solver_set_option(P.PFT_OPT_ONE_STREAM, 0 if a.two_stream else 1)
+    L.pft_solver_set_option(P.PFT_OPT_ONE_STREAM, 0 if a.two_stream else (2 if a.comm_boundary else 1))
     L.pft_solver_set_option(P.PFT_OPT_WAVE, a.wave)
 
     def barrier():
@@ -260,7 +263,8 @@ def main():
                    "gl_static": a.gl_static, "kz": a.kz or "auto", "tile": a.tile, "recompute": not a.no_recompute,
                    "accepted_steps_total": int(sim.system.steps), "t_end": sim.t,
                    "host_boundary": a.host_boundary, "self_exchange": a.self_exchange,
-                   "pipeline": "two-stream" if a.two_stream else "one-stream", "wave": a.wave,
+                   "pipeline": ("two-stream" if a.two_stream else "comm-boundary" if a.comm_boundary
+                                else "one-stream"), "wave": a.wave,
                    "gl_store_skipped": gl_keep,
                    "tiles": ({str(k): ("cache" if v[0] == 0 else f"{2 * v[1]}x{v[2]} cells")
                               for k, v in geo.items()} if geo else None)},

@@ -44,7 +44,8 @@ enum {
 	PFT_OPT_ONE_STREAM = 7, /* N > 1 stage pipeline: 1 (default) = one compute stream (boundary
 	                           launch, the exchange on the comm stream beside the interior sweep,
 	                           wait); 0 = two streams (boundary launch and exchange on the comm
-	                           stream beside the interior sweep) */
+	                           stream beside the interior sweep); 2 = boundary launch and exchange
+	                           on the comm stream, the interior sweep waiting for the launch */
 	PFT_OPT_WAVE = 8        /* one slab, fused path: W > 0 runs a step's five stages as a skewed
 	                           z-wavefront of W-plane launches (chunk c: stage s on planes
 	                           [cW - s + 1, (c+1)W - s + 1)), so each K is read back while it is

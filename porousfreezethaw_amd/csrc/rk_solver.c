@@ -122,7 +122,7 @@ int pft_solver_set_option(int opt, long value)
 		case PFT_OPT_KZ: if(value < 0) return -2; R.opt_kz = (int)value; if(R.slab) pft_slab_set_kz(R.slab, R.opt_kz); return 0;
 		case PFT_OPT_DEVICE: R.opt_dev = (int)value; return 0;
 		case PFT_OPT_TIMING: if(value < 0) return -2; R.opt_timing = (int)value; return 0;
-		case PFT_OPT_ONE_STREAM: R.opt_one_stream = value ? 1 : 0; return 0;
+		case PFT_OPT_ONE_STREAM: if(value < 0 || value > 2) return -2; R.opt_one_stream = (int)value; return 0;
 		case PFT_OPT_WAVE: if(value < 0) return -2; R.opt_wave = (int)value; return 0;
 		case PFT_OPT_RECOMPUTE:
 			R.opt_norecompute = value ? 0 : 1; if(R.slab) pft_slab_set_recompute(R.slab, !R.opt_norecompute); return 0;
@@ -225,6 +225,23 @@ static int do_stage(int stage, double ts, double coef, double h, long * launches
 	   previous interior sweep is done; the interior sweep waits only for the previous stage's
 	   boundary launch. */
 	n3 = R.slab_grid.n3;
+	if(R.opt_one_stream == 2) {
+		/* the boundary launch on the comm stream, its exchange right behind it in stream order (no
+		   cross-stream wait between them, so the priority stream's RCCL kernel is dispatched before
+		   the interior sweep, which waits for the boundary launch by event) */
+		if((rc = pft_slab_order(R.slab, 0))) return rc;          /* after the previous interior sweep */
+		pft_slab_launch_on_comm(R.slab, 1);
+		rc = run1(stage, ts, coef, h, PFT_K_BOUNDARY, 0);
+		pft_slab_launch_on_comm(R.slab, 0);
+		if(rc) return rc;
+		if((rc = pft_slab_boundary_event(R.slab, 0))) return rc; /* recorded behind the boundary launch */
+		if((rc = pft_comm_halo_enqueue_comm(c, out_buf, 0, nfields))) return rc;
+		if((rc = pft_slab_boundary_event(R.slab, 1))) return rc; /* the interior sweep waits for it */
+		if(n3 > 2 && (rc = run1(stage, ts, coef, h, 1, n3-1))) return rc;
+		if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
+		*launches += 2;
+		return 0;
+	}
 	if(R.opt_one_stream) {
 		/* one stream: both boundary planes, their exchange beside the interior sweep, then the
 		   compute stream waits for the exchange */

@@ -190,7 +190,7 @@ def _loopback_run(meta, initial, nprocs, times, mode=0, gl_static=False, flavour
     return out
 
 
-@pytest.mark.parametrize("one_stream", [1, 0])
+@pytest.mark.parametrize("one_stream", [1, 0, 2])
 @pytest.mark.parametrize("nprocs", [2, 4])
 @pytest.mark.parametrize("gl_static", [False, True])
 @pytest.mark.parametrize("flavour", ["default", "fused32", "tile16", "cache"])
@@ -221,7 +221,7 @@ def _self_exchange_comm():
     return comm
 
 
-@pytest.mark.parametrize("one_stream", [1, 0])
+@pytest.mark.parametrize("one_stream", [1, 0, 2])
 @pytest.mark.parametrize("gl_static", [False, True])
 @pytest.mark.parametrize("flavour", ["default", "fusedauto", "fused16", "tile32", "cache"])
 def test_rccl_stage_pipeline_self_exchange_bitwise(gl_static, flavour, one_stream):
