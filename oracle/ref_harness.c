@@ -25,6 +25,11 @@
  *        RK_MPI_SA_solve() to each T_i in turn (like intertrack.c:2283) -> <outdir>/traj.txt
  *        (t, h, steps, steps_total, return code per call, hex floats) and
  *        <outdir>/state<i>.f64 (global interior after call i)
+ *   pft_ref solvex <Params> <outdir> <state.f64> <t0> <h0> <handle_nan> <break_at> <T1> [<T2> ...]
+ *        as solve, with RK_MPI_SA_handle_NAN(handle_nan) (hybrid2.c:138-166) and, when break_at
+ *        >= 0, a Service_Callback (hybrid2.c:670-705) that logs every call (steps, t, h) to
+ *        <outdir>/cb.txt and returns 1 on its break_at-th call (0 = never); traj.txt rows gain
+ *        RK_MPI_SA_check_NAN()
  */
 
 #include "common.h"
@@ -257,6 +262,18 @@ static void eval_ic(void)
 	}
 }
 
+/* solvex's Service_Callback: log every call, interrupt on the break_at-th */
+static FILE * cb_file;
+static long cb_calls, cb_break_at;
+
+static int logging_callback(FLOAT final_time, RK_MPI_S_SOLUTION * s)
+{
+	(void)final_time;
+	cb_calls++;
+	if(cb_file) fprintf(cb_file, "%ld %a %a\n", s->steps, s->t, s->h);
+	return (cb_break_at > 0 && cb_calls == cb_break_at) ? 1 : 0;
+}
+
 static RK_RightHandSide (*pick_meta(void))()
 {
 	/* intertrack.c:2131-2135 */
@@ -299,7 +316,9 @@ int main(int argc, char ** argv)
 		sprintf(path, "%s/rhs.f64", argv[3]); gather_write(K, path);
 		sprintf(path, "%s/w_rank%d.f64", argv[3], MPIrank);
 		{ FILE * f = fopen(path, "wb"); fwrite(solution, sizeof(FLOAT), VAR_COUNT*subgridSIZE, f); fclose(f); }
-	} else if(!strcmp(argv[1], "solve")) {
+	} else if(!strcmp(argv[1], "solve") || !strcmp(argv[1], "solvex")) {
+		const int ext = !strcmp(argv[1], "solvex");
+		const int first_T = ext ? 9 : 7;
 		double * g;
 		int c = 0, j, k, call;
 		int n_chunks = VAR_COUNT*n2*n3;
@@ -322,12 +341,22 @@ int main(int argc, char ** argv)
 			if(RK_MPI_SA_init(VAR_COUNT*subgridSIZE, MPI_COMM_WORLD, 0)) MPI_Abort(MPI_COMM_WORLD, 8);
 			if(RK_MPI_SA_check_mem(&md)) MPI_Abort(MPI_COMM_WORLD, 9);
 			if(MPIrank==0) { sprintf(path, "%s/traj.txt", argv[3]); tf = fopen(path, "w"); }
-			for(call=7; call<argc; call++) {
+			if(ext) {
+				RK_MPI_SA_handle_NAN(atoi(argv[7]));
+				cb_break_at = atol(argv[8]);
+				if(cb_break_at >= 0) {
+					sys.Service_Callback = logging_callback;
+					if(MPIrank==0) { sprintf(path, "%s/cb.txt", argv[3]); cb_file = fopen(path, "w"); }
+				}
+			}
+			for(call=first_T; call<argc; call++) {
 				int rc = RK_MPI_SA_solve(strtod(argv[call], NULL), &sys);
-				if(tf) fprintf(tf, "%a %a %ld %ld %d\n", sys.t, sys.h, sys.steps, sys.steps_total, rc);
-				sprintf(path, "%s/state%d.f64", argv[3], call-7); gather_write(solution, path);
+				if(tf && ext) fprintf(tf, "%a %a %ld %ld %d %d\n", sys.t, sys.h, sys.steps, sys.steps_total, rc, RK_MPI_SA_check_NAN());
+				else if(tf) fprintf(tf, "%a %a %ld %ld %d\n", sys.t, sys.h, sys.steps, sys.steps_total, rc);
+				sprintf(path, "%s/state%d.f64", argv[3], call-first_T); gather_write(solution, path);
 			}
 			if(tf) fclose(tf);
+			if(cb_file) fclose(cb_file);
 			RK_MPI_SA_cleanup();
 		}
 	} else {

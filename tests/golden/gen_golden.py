@@ -17,6 +17,8 @@ Cases (SURVEY.md section 4.2 KATs 1-4):
            RHS for all modes on 1 and 4 ranks (ranks hold 8/8/7/7 planes), plus every
            rank's padded input array after bcond_setup+sync_solution (boundary KAT),
            and single-step solves (accepted and rejected-first).
+  ctl      control-flow KATs on g20: NaN give-up (3 variants), NaN retries then recovery, and
+           a Service_Callback break + resume, with the (steps, t, h) the callback saw per step
   g100     BASELINE configs[0]: default Params at grid_nodes 100 (50x50x100): parameters, the
            SHA-256 of the IC and of a mode-0 trajectory to two snapshot times (checked identical
            on 2 ranks), plus the middle and top z-planes of each state (a state is 6 MB).
@@ -198,6 +200,72 @@ def case_g100():
     return arrays, meta
 
 
+def traj_ext(out, ncalls, shape):
+    """solvex rows: t, h, steps, steps_total, rc, check_NAN; cb.txt rows: steps, t, h"""
+    rows = [l.split() for l in open(os.path.join(out, "traj.txt"))]
+    meta = [[float.fromhex(r[0]).hex(), float.fromhex(r[1]).hex(), int(r[2]), int(r[3]), int(r[4]), int(r[5])]
+            for r in rows]
+    cb = []
+    if os.path.exists(os.path.join(out, "cb.txt")):
+        cb = [[int(r[0]), float.fromhex(r[1]).hex(), float.fromhex(r[2]).hex()]
+              for r in (l.split() for l in open(os.path.join(out, "cb.txt")))]
+    states = [load(os.path.join(out, f"state{i}.f64"), shape) for i in range(ncalls)]
+    return meta, cb, states
+
+
+def case_ctl():
+    """Control-flow KATs of RK_MPI_SA_solve (hybrid2.c) on the g20 grid, mode 0, run through the
+    reference's solvex harness command:
+      nan_giveup_*  a NaN in the state with RK_MPI_SA_handle_NAN(1): h/10 retries until
+                    h/(T-t) < 1e-11, return -4 (hybrid2.c:464-504, 624-646), for three (t0, h0, T)
+      nan_retry     h0 = 1e8 s: the first attempts overflow to inf/NaN in the stage values, h/10
+                    retries until the error norm is finite, then ordinary steps; a Service_Callback
+                    logs (steps, t, h) after every accepted step and interrupts at the 10th
+      cb_break      h0 = 1, T = 36: the callback interrupts at its 25th call (return 1, t and
+                    h = new_h left in the system, hybrid2.c:697-705), the second call resumes to
+                    T; the log holds every accepted step of both calls"""
+    arrays, meta = {}, {"case": "ctl", "source": "reference Params, grid_nodes 20, solvex"}
+    w = Work({"grid_nodes": 20})
+    try:
+        out = w.run(1, "setup")
+        p = read_params(out)
+        shape = (3, p["n3"], p["n2"], p["n1"])
+        ic = load(os.path.join(out, "ic.f64"), shape)
+        meta["params"] = hexify(p)
+        arrays["ic"] = ic
+        runs = {}
+        nan_ic = ic.copy()
+        nan_ic[0, 5, 5, 5] = np.nan
+        inf_ic = ic.copy()
+        inf_ic[1, 13, 2, 7] = np.inf
+        # name: (state, t0, h0, handle_nan, break_at, [T...])
+        spec = {
+            "nan_giveup_a": (nan_ic, 0.0, 1.0, 1, -1, [36.0]),
+            "nan_giveup_b": (nan_ic, 100.0, 5.0, 1, -1, [1e5]),
+            "nan_giveup_c": (inf_ic, 7.0, 0.25, 1, -1, [7.5]),
+            "nan_retry": (ic, 0.0, 1e8, 1, 10, [1e9]),
+            "cb_break": (ic, 0.0, 1.0, 0, 25, [36.0, 36.0]),
+        }
+        for name, (st, t0, h0, hn, brk, Ts) in spec.items():
+            sp = os.path.join(w.dir, name + ".f64")
+            st.tofile(sp)
+            o = w.run(1, "solvex", sp, t0, h0, hn, brk, *Ts)
+            tm, cb, states = traj_ext(o, len(Ts), shape)
+            if name in ("nan_retry", "cb_break"):
+                o3 = w.run(3, "solvex", sp, t0, h0, hn, brk, *Ts)
+                tm3, cb3, states3 = traj_ext(o3, len(Ts), shape)
+                assert tm == tm3 and cb == cb3 and all(np.array_equal(a, b) for a, b in zip(states, states3))
+            runs[name] = {"t0": t0, "h0": h0, "handle_nan": hn, "break_at": brk, "T": Ts, "traj": tm, "cb": cb}
+            if name.startswith("nan_giveup"):
+                arrays[name + "_ic"] = st
+            for i, s in enumerate(states):
+                arrays[f"{name}_state{i}"] = s
+        meta["runs"] = runs
+    finally:
+        w.close()
+    return arrays, meta
+
+
 def case_ragged():
     arrays, meta = {}, {"case": "ragged", "source": "reference Params, L1=0.036 L2=0.024 grid_nodes 30"}
     rep = {"L1": 0.036, "L2": 0.024, "grid_nodes": 30}
@@ -247,7 +315,7 @@ def case_ragged():
 def main():
     if not os.path.exists(PFT_REF):
         sys.exit("build the reference harness first: make -C oracle ref")
-    cases = {"g20": case_g20, "ragged": case_ragged, "g100": case_g100}
+    cases = {"g20": case_g20, "ragged": case_ragged, "g100": case_g100, "ctl": case_ctl}
     for name in sys.argv[1:] or list(cases):
         arrays, meta = cases[name]()
         name = meta["case"]

@@ -307,42 +307,6 @@ def test_host_staged_path_with_foreign_rhs():
     sim.close()
 
 
-def test_service_callback_break_and_resume():
-    """Service_Callback returning nonzero interrupts solve() with return code 1 (hybrid2.c:684-705);
-    resuming reaches the same final state as an uninterrupted run"""
-    meta, A = O.load_case("g20")
-    T = meta["traj_times"][0]
-    sim, Pm, info = make_sim(meta, A["traj_m0_ic"])
-    calls = []
-
-    @P.SERVICE_FN
-    def cb(final, s):
-        calls.append(s.contents.steps)
-        return 1 if len(calls) == 25 else 0
-
-    sim.system.Service_Callback = C.cast(cb, C.c_void_p).value
-    assert sim.solve(T) == 1
-    assert sim.system.steps == 25
-    assert sim.solve(T) == 0
-    assert sim.t == T
-    sim.close()
-
-
-def test_nan_handling_gives_up():
-    meta, A = O.load_case("g20")
-    ic = A["traj_m0_ic"].copy()
-    ic[0, 5, 5, 5] = np.nan
-    sim, Pm, info = make_sim(meta, ic)
-    P.lib().RK_MPI_SA_handle_NAN(1)
-    try:
-        rc = sim.lib.RK_MPI_SA_solve(36.0, C.byref(sim.system))
-        assert rc == -4
-        assert sim.lib.RK_MPI_SA_check_NAN() == 1
-    finally:
-        P.lib().RK_MPI_SA_handle_NAN(0)
-        sim.close()
-
-
 def _full_size_case():
     from porousfreezethaw_amd import params as PR
     base = PR.default_params(grid_nodes=400, calc_mode=0)
