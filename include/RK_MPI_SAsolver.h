@@ -78,7 +78,10 @@ typedef struct __struct_RK_MPI_S_SOLUTION {
 	long steps_total;                                  /* attempted steps */
 } RK_MPI_S_SOLUTION;
 
-/* 0 ok, -1 no memory, -2 bad size, -3 already initialised, -4 communicator not initialised */
+/* 0 ok, -1 no memory, -2 bad size, -3 already initialised, -4 communicator not initialised.
+   libpft allocates the solver's device buffers here (the fused path's slab when the model is
+   configured and max_block_size holds its block, else the host-staged arrays): -1 when that
+   fails (HBM exhausted, or no HIP device).  -4 also for a `comm` other than MPI_COMM_WORLD. */
 int RK_MPI_SA_init(int max_block_size, MPI_Comm comm, int master_rank);
 /* 0 ok, -3 not initialised */
 int RK_MPI_SA_cleanup(void);
@@ -87,7 +90,9 @@ int RK_MPI_SA_check_NAN();
 /* 0 ok, -3 not initialised, -5 beyond max_block_size, -6 bad chunk order/size, -7 no chunks */
 int RK_MPI_SA_check_mem(RK_MEM_DIST * n);
 /* 0 ok, 1 interrupted by Service_Callback, -2 bad system, -3 not initialised,
-   -4 NaN persists (NaN handling on), -5 last chunk beyond max_block_size, -6 error on another rank */
+   -4 NaN persists (NaN handling on), -5 last chunk beyond max_block_size, -6 error on another rank,
+   and one code the reference does not have: -7 device / communication failure (HIP or RCCL,
+   PFT_SOLVE_DEVICE_ERROR in pft_solver.h, details from pft_solver_last_status()) */
 int RK_MPI_SA_solve(FLOAT final_time, RK_MPI_S_SOLUTION * system);
 
 #ifdef __cplusplus

@@ -79,5 +79,7 @@ static int pft_adapter_cleanup(void)
 /* the driver's calls below this point reach the adapter */
 #define AllocPrecalcData() pft_adapter_alloc()
 #define PrecalculateData(m) pft_adapter_precalc(m)
-#define RK_MPI_SA_init(size, comm, master) RK_MPI_SA_init((size), (comm), 0)
+/* libpft's communicator stands for the driver's MPI_COMM_WORLD; its handle is MPICH's value, passed
+   as such whatever the MPI library's MPI_Comm type is */
+#define RK_MPI_SA_init(size, comm, master) RK_MPI_SA_init((size), (MPI_Comm)(long)0x44000000, 0)
 #define RK_MPI_SA_cleanup() pft_adapter_cleanup()

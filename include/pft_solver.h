@@ -24,8 +24,19 @@ extern "C" {
    continues the identical trajectory) and the flags above. */
 int pft_solve_ex(FLOAT final_time, RK_MPI_S_SOLUTION * system, long max_steps_total, int flags);
 
-/* copy the device-resident x back into system->x (host layout) */
+/* copy the device-resident x back into system->x (host layout): after a pft_solve_ex call with
+   PFT_SOLVE_KEEP_DEVICE, or from inside a Service_Callback on the fused path -- there the state
+   lives on the device and system->x is only refreshed when solve returns, so a callback that
+   reads x (a snapshot, say) downloads it first.  The reference's RKService (intertrack.c:1072-1116)
+   reads only t and h. */
 int pft_solver_download(RK_MPI_S_SOLUTION * system);
+
+/* RK_MPI_SA_solve / pft_solve_ex return value added to the reference's codes
+   (RK_MPI_SAsolver.h:384-392): a HIP or RCCL failure (out of device memory, a device fault, a
+   lost peer).  pft_solver_last_status() gives the raw status (-1000 - hipError_t, -3000 -
+   ncclResult_t, -1 host allocation) and pft_hip_last_error() the HIP error text. */
+#define PFT_SOLVE_DEVICE_ERROR  (-7)
+int pft_solver_last_status(void);
 
 enum {
 	PFT_OPT_GL_STATIC = 1,  /* 1: exploit dgl == 0 (equation.c:731,874): gl neither stored in K
@@ -46,10 +57,14 @@ enum {
 	                           wait); 0 = two streams (boundary launch and exchange on the comm
 	                           stream beside the interior sweep); 2 = boundary launch and exchange
 	                           on the comm stream, the interior sweep waiting for the launch */
-	PFT_OPT_WAVE = 8        /* one slab, fused path: W > 0 runs a step's five stages as a skewed
+	PFT_OPT_WAVE = 8,       /* one slab, fused path: W > 0 runs a step's five stages as a skewed
 	                           z-wavefront of W-plane launches (chunk c: stage s on planes
 	                           [cW - s + 1, (c+1)W - s + 1)), so each K is read back while it is
 	                           still in the Infinity Cache; 0 (default) = one launch per stage */
+	PFT_OPT_LAZY_ALLOC = 9  /* 1: RK_MPI_SA_init only checks its arguments and the device buffers
+	                           are allocated by the first solve (host-only checks of the ABI);
+	                           0 (default): RK_MPI_SA_init allocates them, as hybrid2.c:101-112
+	                           allocates K1..K5 and aux, and returns -1 when that fails */
 };
 int pft_solver_set_option(int opt, long value);
 

@@ -30,6 +30,8 @@ PFT_SOLVE_KEEP_DEVICE, PFT_SOLVE_REUSE_DEVICE = 1, 2
 PFT_OPT_GL_STATIC, PFT_OPT_KZ, PFT_OPT_DEVICE, PFT_OPT_TIMING, PFT_OPT_TILE, PFT_OPT_RECOMPUTE = 1, 2, 3, 4, 5, 6
 PFT_OPT_ONE_STREAM = 7
 PFT_OPT_WAVE = 8
+PFT_OPT_LAZY_ALLOC = 9
+PFT_SOLVE_DEVICE_ERROR = -7
 MPI_COMM_WORLD = 0x44000000
 
 # every function of the public headers, for the "library exports its ABI" check
@@ -99,6 +101,7 @@ def lib():
         L.pft_solver_download.argtypes = [C.POINTER(RK_MPI_S_SOLUTION)]
         L.pft_solver_set_option.argtypes = [C.c_int, C.c_long]
         L.pft_solver_get_stats.argtypes = [C.POINTER(pft_solver_stats)]
+        L.pft_solver_last_status.restype = C.c_int
         L.pft_solver_slab.restype = C.c_void_p
         L.pft_slab_tile_geometry.argtypes = [C.c_void_p, C.c_int, ip, ip]
         L.pft_decompose.argtypes = [C.c_int, C.c_int, C.c_int, ip, ip]

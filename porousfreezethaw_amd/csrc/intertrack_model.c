@@ -384,23 +384,27 @@ int pft_model_ic_default(FLOAT * w)
 /* implemented in rk_solver.c: evaluate the device RHS on a host array */
 int pft_solver_eval_rhs(FLOAT t, const FLOAT * w, FLOAT * dw);
 
+/* The reference's right-hand side cannot fail (void, equation.c:566); a device failure here leaves
+   NaN in every entry of dw, which a caller's NaN handling (RK_MPI_SA_handle_NAN) sees, and the
+   status in pft_solver_last_status() / the text in pft_hip_last_error(). */
+static void rhs_failed(const char * who, FLOAT * dw)
+{
+	long i, n = PFT_VAR_COUNT * M.S;
+	for(i = 0; i < n; i++) dw[i] = NAN;
+	fprintf(stderr, "libpft: %s: device evaluation failed (%s)\n", who, pft_hip_last_error());
+}
+
 void f_generic_model01(FLOAT t, const FLOAT * w, FLOAT * dw_dt)
 {
 	/* the reference writes the ghost layers of its input (equation.c:622-626) */
 	bcond_setup(t, (FLOAT*)w);
-	if(pft_solver_eval_rhs(t, w, dw_dt)) {
-		fprintf(stderr, "libpft: f_generic_model01: device evaluation failed (%s)\n", pft_hip_last_error());
-		abort();
-	}
+	if(pft_solver_eval_rhs(t, w, dw_dt)) rhs_failed("f_generic_model01", dw_dt);
 }
 
 void f_generic_model2(FLOAT t, const FLOAT * w, FLOAT * dw_dt)
 {
 	bcond_setup(t, (FLOAT*)w);
-	if(pft_solver_eval_rhs(t, w, dw_dt)) {
-		fprintf(stderr, "libpft: f_generic_model2: device evaluation failed (%s)\n", pft_hip_last_error());
-		abort();
-	}
+	if(pft_solver_eval_rhs(t, w, dw_dt)) rhs_failed("f_generic_model2", dw_dt);
 }
 
 static RK_RightHandSide mf_generic(void)

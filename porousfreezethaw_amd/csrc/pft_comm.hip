@@ -54,6 +54,7 @@ static __thread pft_comm* g_current = nullptr;
     hipError_t e_ = (x);                                                   \
     if (e_ != hipSuccess) {                                                \
       fprintf(stderr, "pft_comm: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+      (void)hipGetLastError();                                             \
       return -1000 - (int)e_;                                              \
     }                                                                      \
   } while (0)

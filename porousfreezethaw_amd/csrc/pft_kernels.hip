@@ -99,6 +99,9 @@ static __thread char g_err[256];
 static int fail(hipError_t e, const char* what)
 {
   snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+  // the failed call also left e as the thread's "last error": reset it, or the next launch's
+  // hipGetLastError() check would report it again (e.g. after an allocation that found the HBM full)
+  (void)hipGetLastError();
   return -(int)e - 1000;
 }
 #define HIPCHK(x)                                  \
@@ -1338,7 +1341,9 @@ static int ensure_staging(pft_slab* s)
 
 int pft_slab_upload_host(pft_slab* s, int which, const double* host_padded)
 {
-  s->gl_keep = 0;        // X and XN may differ now: the caller re-establishes it
+  // X and XN may differ now: the caller re-establishes it (an upload of a stage buffer, e.g. A0
+  // for a host-side RHS evaluation, leaves it alone)
+  if (which == PFT_BUF_X || which == PFT_BUF_XN) s->gl_keep = 0;
   int rc = ensure_staging(s);
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(s->staging, host_padded, sizeof(double) * 3 * (size_t)s->S, hipMemcpyHostToDevice,
@@ -1540,6 +1545,9 @@ int pft_slab_stage_fields(const pft_slab* s, int stage)
   if (stage < 1 || stage > 6) return -2;
   if (s->d.gl_static) return 2;
   if (slab_kind(s) == KFUSED && PFT_GLK_LITERAL && stage != 5) return 2;
+  // stage 5 with gl_keep (agreed by every rank, rk_solver.c): gl's x(t+h) is not stored; the
+  // neighbours' XN gl ghost planes already equal X's (both exchanged at upload)
+  if (stage == 5 && pft_slab_get_gl_keep(s) && slab_kind(s) == KFUSED) return 2;
   return 3;
 }
 

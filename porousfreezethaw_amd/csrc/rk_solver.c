@@ -41,7 +41,10 @@ typedef struct {
 	double *h_k, *h_aux; int h_cap;
 	/* options */
 	int opt_gls, opt_kz, opt_dev, opt_timing, opt_tile, opt_norecompute, opt_one_stream, opt_wave;
+	int opt_lazy;               /* PFT_OPT_LAZY_ALLOC: device buffers at the first solve, not at init */
 	int tstep;                  /* this attempted step's stages are timed (every opt_timing-th) */
+	int last_status;            /* raw status of the last device / communication failure */
+	int in_callback;            /* inside Service_Callback on the fused path (x is on the device) */
 	pft_solver_stats stats;
 } solver_state;
 
@@ -59,18 +62,46 @@ static pft_comm * comm(void)
 /* ---------------------------------------------------------------------------------------- */
 /* lifecycle, hybrid2.c:72-212 */
 
+static int ensure_slab(void);
+static int alloc_staged(void);
+static void free_staged(void);
+
+/* the device buffers RK_MPI_SA_init allocates (hybrid2.c:101-112 allocates K1, K3, K4, K5, aux):
+   the fused path's slab when the model is configured and max_block_size holds its intertrack
+   block (intertrack.c:2192 passes 3 * subgridSIZE), otherwise the host-staged path's arrays */
+static int alloc_at_init(void)
+{
+	pft_grid g;
+	int rc;
+	if(pft_model_get_grid(&g) == 0) {
+		const long S = (g.n1 + 2L*PFT_BCOND_THICKNESS) * (g.n2 + 2L*PFT_BCOND_THICKNESS) *
+		               (g.n3 + 2L*PFT_BCOND_THICKNESS);
+		if(R.max_n >= PFT_VAR_COUNT*S) return ensure_slab();
+	}
+	rc = alloc_staged();
+	return rc;
+}
+
 int RK_MPI_SA_init(int max_block_size, MPI_Comm comm_handle, int master_rank)
 {
 	pft_comm * c = comm();
-	(void)comm_handle;            /* the ranks are those of the pft communicator (pft_comm.h) */
-	if(!c) return -4;                                       /* :95 */
+	int rc;
+	/* :95; the ranks are those of the pft communicator (pft_comm.h), which stands for the
+	   driver's MPI_COMM_WORLD -- any other communicator is unknown to libpft */
+	if(!c || comm_handle != PFT_COMM_WORLD) return -4;
 	if(R.max_n) return -3;                                  /* :98 */
 	if(max_block_size <= 0) return -2;                      /* :99 */
 	if(master_rank < 0 || master_rank >= pft_comm_size(c)) return -4;
-	/* device buffers are sized by the path the first solve() takes (:101-112) */
 	R.max_n = max_block_size;                               /* :114-118 */
 	R.last_nan = 0;
 	R.master = master_rank;
+	if(!R.opt_lazy && (rc = alloc_at_init())) {             /* :101-112: -1, not enough memory */
+		R.last_status = rc;
+		if(R.slab) { pft_comm_attach(comm(), NULL); pft_slab_destroy(R.slab); R.slab = NULL; }
+		free_staged();
+		R.max_n = 0;
+		return -1;
+	}
 	return 0;
 }
 
@@ -124,6 +155,7 @@ int pft_solver_set_option(int opt, long value)
 		case PFT_OPT_TIMING: if(value < 0) return -2; R.opt_timing = (int)value; return 0;
 		case PFT_OPT_ONE_STREAM: if(value < 0 || value > 2) return -2; R.opt_one_stream = (int)value; return 0;
 		case PFT_OPT_WAVE: if(value < 0) return -2; R.opt_wave = (int)value; return 0;
+		case PFT_OPT_LAZY_ALLOC: R.opt_lazy = value ? 1 : 0; return 0;
 		case PFT_OPT_RECOMPUTE:
 			R.opt_norecompute = value ? 0 : 1; if(R.slab) pft_slab_set_recompute(R.slab, !R.opt_norecompute); return 0;
 		case PFT_OPT_TILE:
@@ -134,6 +166,7 @@ int pft_solver_set_option(int opt, long value)
 }
 
 int pft_solver_get_stats(pft_solver_stats * st) { *st = R.stats; return 0; }
+int pft_solver_last_status(void) { return R.last_status; }
 pft_slab * pft_solver_slab(void) { return R.slab; }
 
 /* ---------------------------------------------------------------------------------------- */
@@ -325,6 +358,9 @@ typedef struct {
 	int delta_mode, handle_nan, any_cb;
 } solve_bcast;
 
+static int run_staged(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast * B, int command,
+                      long max_steps_total, int flags);
+
 static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast * B, int command,
                      long max_steps_total, int flags, const double * em)
 {
@@ -332,7 +368,7 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	const int rank = pft_comm_rank(c), nprocs = pft_comm_size(c);
 	double t = B->t, h = B->h, new_h = 0.0, h2, h3, h6, h8, eps;
 	const double final_time = B->final_time, delta = B->delta, h_min = B->h_min;
-	int nonfinite, rc, ret = 0;
+	int nonfinite, rc, ret = 0, to_host = 0;
 	long attempted = 0, launches = 0;
 	int spec, k1_valid = 0;               /* K1 holds f(t, x) for the current t and x */
 
@@ -341,7 +377,12 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	if(!(flags & PFT_SOLVE_REUSE_DEVICE) || !R.device_valid) {
 		if((rc = pft_slab_upload_host(R.slab, PFT_BUF_X, system->x))) return rc;
 		if((rc = pft_slab_upload_host(R.slab, PFT_BUF_XN, system->x))) return rc;
-		pft_slab_set_gl_keep(R.slab, gl_clean(system->x));
+		{
+			/* every rank must agree: the stage-5 exchange carries gl only when some rank stores it */
+			long long unclean = !gl_clean(system->x);
+			if(nprocs > 1 && (rc = pft_comm_allreduce_max_i64(c, &unclean))) return rc;
+			pft_slab_set_gl_keep(R.slab, !unclean);
+		}
 		if(nprocs > 1) {
 			if((rc = pft_comm_halo(c, PFT_BUF_X, 0, 3))) return rc;
 			if((rc = pft_comm_halo(c, PFT_BUF_XN, 0, 3))) return rc;
@@ -412,9 +453,13 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 				else k1_valid = 0;
 				system->steps++;
 				if(system->Service_Callback != NULL) {                           /* :676-685 */
+					/* x stays on the device: a callback that reads it calls
+					   pft_solver_download(system) first (pft_solver.h) */
 					system->t = t;
 					system->h = h;
+					R.in_callback = 1;
 					if(system->Service_Callback(final_time, system)) command |= RKA_CMD_BREAK;
+					R.in_callback = 0;
 				}
 				if(nprocs > 1 && B->any_cb) pft_comm_bcast(c, &command, sizeof(int), R.master);   /* :690 */
 				if(command & RKA_CMD_FINISHED) break;                            /* :695 */
@@ -425,7 +470,9 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 					break;
 				}
 				f = system->meta_f();                                            /* :732 */
-				if(!pft_model_is_device_rhs(f)) { ret = -2; break; }
+				/* another right-hand side from the next step on: the state leaves the device
+				   and the loop continues on the host-staged path (below) */
+				if(!pft_model_is_device_rhs(f)) to_host = 1;
 			}
 			if(command & RKA_CMD_NEXTFINISH) {                                   /* :743-761 */
 				system->h = new_h;
@@ -443,6 +490,7 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 			ret = 2;
 			break;
 		}
+		if(to_host) break;
 	}
 	(void)rank;
 	/* join the comm stream (the last boundary launch and exchange) before the state leaves */
@@ -453,15 +501,24 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	R.device_valid = 1;
 	R.stats.kernel_launches = launches;
 	R.stats.steps_total = attempted;
-	if(!(flags & PFT_SOLVE_KEEP_DEVICE)) {
+	if(!(flags & PFT_SOLVE_KEEP_DEVICE) || to_host) {
 		if((rc = pft_slab_download_host(R.slab, PFT_BUF_X, system->x))) return rc;
+	}
+	if(to_host) {
+		/* meta_f() returned a right-hand side that is not libpft's: carry on from t, h and the
+		   pending command with it, on the host-staged path (hybrid2.c:732 keeps integrating with
+		   the new f) */
+		R.device_valid = 0;
+		B->t = t;
+		B->h = h;
+		return run_staged(system, f, B, command, max_steps_total > 0 ? max_steps_total - attempted : 0, flags);
 	}
 	return ret;
 }
 
 int pft_solver_download(RK_MPI_S_SOLUTION * system)
 {
-	if(!R.slab || !R.device_valid || !system || !system->x) return -2;
+	if(!R.slab || !(R.device_valid || R.in_callback) || !system || !system->x) return -2;
 	return pft_slab_download_host(R.slab, PFT_BUF_X, system->x);
 }
 
@@ -470,30 +527,37 @@ int pft_solver_eval_rhs(FLOAT t, const FLOAT * w, FLOAT * dw)
 	/* f(t, w, dw) on host arrays: stage w into A0, exchange its boundary planes, K into K1 */
 	pft_comm * c = comm();
 	int rc;
-	if((rc = ensure_slab())) return rc;
-	if((rc = pft_slab_upload_host(R.slab, PFT_BUF_A0, w))) return rc;
-	if(pft_comm_size(c) > 1 && (rc = pft_comm_halo(c, PFT_BUF_A0, 0, 3))) return rc;
-	if((rc = pft_slab_rhs(R.slab, PFT_BUF_A0, PFT_BUF_K1, t))) return rc;
-	return pft_slab_download_host(R.slab, PFT_BUF_K1, dw);
+	if(!(rc = ensure_slab()) && !(rc = pft_slab_upload_host(R.slab, PFT_BUF_A0, w)) &&
+	   !(pft_comm_size(c) > 1 && (rc = pft_comm_halo(c, PFT_BUF_A0, 0, 3))) &&
+	   !(rc = pft_slab_rhs(R.slab, PFT_BUF_A0, PFT_BUF_K1, t)))
+		rc = pft_slab_download_host(R.slab, PFT_BUF_K1, dw);
+	if(rc) R.last_status = rc;
+	return rc;
 }
 
 /* ---------------------------------------------------------------------------------------- */
 /* host-staged path: any right-hand side, combines on the GPU over the chunk table */
 
+static int alloc_staged(void)
+{
+	int rc;
+	if(R.d_cap >= R.max_n) return 0;
+	free_staged();
+	if((rc = pft_flat_alloc(&R.d_x, R.max_n)) || (rc = pft_flat_alloc(&R.d_k1, R.max_n)) ||
+	   (rc = pft_flat_alloc(&R.d_k3, R.max_n)) || (rc = pft_flat_alloc(&R.d_k4, R.max_n)) ||
+	   (rc = pft_flat_alloc(&R.d_k5, R.max_n)) || (rc = pft_flat_alloc(&R.d_aux, R.max_n)) ||
+	   (rc = pft_flat_alloc(&R.d_eps, 2))) return rc;
+	R.d_cap = R.max_n;
+	R.h_k = (double*)calloc(R.max_n, sizeof(double));
+	R.h_aux = (double*)calloc(R.max_n, sizeof(double));
+	if(!R.h_k || !R.h_aux) return -1;
+	return 0;
+}
+
 static int ensure_staged(const RK_MEM_DIST * n)
 {
 	int rc;
-	if(R.d_cap < R.max_n) {
-		free_staged();
-		if((rc = pft_flat_alloc(&R.d_x, R.max_n)) || (rc = pft_flat_alloc(&R.d_k1, R.max_n)) ||
-		   (rc = pft_flat_alloc(&R.d_k3, R.max_n)) || (rc = pft_flat_alloc(&R.d_k4, R.max_n)) ||
-		   (rc = pft_flat_alloc(&R.d_k5, R.max_n)) || (rc = pft_flat_alloc(&R.d_aux, R.max_n)) ||
-		   (rc = pft_flat_alloc(&R.d_eps, 2))) return rc;
-		R.d_cap = R.max_n;
-		R.h_k = (double*)calloc(R.max_n, sizeof(double));
-		R.h_aux = (double*)calloc(R.max_n, sizeof(double));
-		if(!R.h_k || !R.h_aux) return -1;
-	}
+	if((rc = alloc_staged())) return rc;
 	if(R.d_nch < n->n_chunks) {
 		pft_dev_free(R.d_cs); pft_dev_free(R.d_cz); pft_flat_free(R.d_cm);
 		if((rc = pft_dev_alloc((void**)&R.d_cs, sizeof(int)*n->n_chunks)) ||
@@ -594,8 +658,15 @@ static int run_staged(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcas
 				t += h;
 				if((rc = pft_flat_combine(6, nch, R.d_cs, R.d_cz, R.d_cm, h3, h, R.d_x, R.d_k1, R.d_k3, R.d_k3,
 				                          R.d_k4, R.d_k5, R.d_x, R.d_eps, NULL))) return rc;    /* :657-668 */
-				/* the right-hand side of the next step reads the host x */
-				if((rc = pft_flat_d2h(x, R.d_x, R.max_n, NULL)) || (rc = pft_stream_sync(NULL))) return rc;
+				/* the right-hand side of the next step reads the host x: only the chunks (the
+				   unknowns) come back, the ghost values the last f(t, x) wrote stay (the
+				   reference updates x in place, hybrid2.c:657-668) */
+				if((rc = pft_flat_d2h(R.h_aux, R.d_x, R.max_n, NULL)) || (rc = pft_stream_sync(NULL))) return rc;
+				{
+					int ch;
+					for(ch = 0; ch < nch; ch++)
+						memcpy(x + n->chunk_start[ch], R.h_aux + n->chunk_start[ch], sizeof(double)*n->chunk_size[ch]);
+				}
 				system->steps++;
 				if(system->Service_Callback != NULL) {
 					system->t = t;
@@ -674,14 +745,23 @@ int pft_solve_ex(FLOAT final_time, RK_MPI_S_SOLUTION * system, long max_steps_to
 	R.stats.nprocs = pft_comm_size(c);
 	R.stats.rank = rank;
 
-	if(pft_model_is_device_rhs(f) && system->DDLBF_Rearrange == NULL) {
+	{
+		int rc;
 		double em[3];
-		if(canonical_chunks(n, em)) {
-			int rc = run_fused(system, f, &B, command, max_steps_total, flags, em);
-			return rc;
+		if(pft_model_is_device_rhs(f) && system->DDLBF_Rearrange == NULL && canonical_chunks(n, em))
+			rc = run_fused(system, f, &B, command, max_steps_total, flags, em);
+		else
+			rc = run_staged(system, f, &B, command, max_steps_total, flags);
+		/* a HIP or RCCL failure (out of device memory, a lost peer, ...) is reported as
+		   PFT_SOLVE_DEVICE_ERROR; the raw status stays in pft_solver_last_status() and the HIP
+		   text in pft_hip_last_error() */
+		if(rc <= -1000 || rc == -1) {
+			R.last_status = rc;
+			R.device_valid = 0;
+			return PFT_SOLVE_DEVICE_ERROR;
 		}
+		return rc;
 	}
-	return run_staged(system, f, &B, command, max_steps_total, flags);
 }
 
 int RK_MPI_SA_solve(FLOAT final_time, RK_MPI_S_SOLUTION * system)

@@ -114,11 +114,26 @@ def test_initial_condition_bitwise():
         assert np.array_equal(np.concatenate(parts, axis=1), A["ic"]), nprocs
 
 
+def test_init_allocates_and_reports_no_memory():
+    """RK_MPI_SA_init allocates the device buffers (hybrid2.c:101-112): on this CPU-only host
+    there is no device memory, so it returns -1 and leaves the solver uninitialised; an unknown
+    communicator is -4 (hybrid2.c:95)"""
+    L = P.lib()
+    if P.device_count() > 0:
+        pytest.skip("a HIP device is visible: the no-memory case is the GPU test's")
+    assert L.RK_MPI_SA_init(100, P.MPI_COMM_WORLD + 1, 0) == -4
+    assert L.RK_MPI_SA_init(100, P.MPI_COMM_WORLD, 0) == -1
+    assert L.pft_solver_last_status() <= -1000          # the HIP error behind it
+    assert L.RK_MPI_SA_cleanup() == -3
+
+
 def test_solver_argument_codes():
     L = P.lib()
+    assert L.pft_solver_set_option(P.PFT_OPT_LAZY_ALLOC, 1) == 0   # argument checks only
     assert L.RK_MPI_SA_cleanup() == -3
     mem = P.RK_MEM_DIST(0, None, None, None)
     assert L.RK_MPI_SA_init(0, P.MPI_COMM_WORLD, 0) == -2
+    assert L.RK_MPI_SA_init(100, P.MPI_COMM_WORLD, 5) == -4      # master rank outside the communicator
     assert L.RK_MPI_SA_init(100, P.MPI_COMM_WORLD, 0) == 0
     assert L.RK_MPI_SA_init(100, P.MPI_COMM_WORLD, 0) == -3
     assert L.RK_MPI_SA_check_mem(C.byref(mem)) == -7
@@ -150,3 +165,10 @@ def test_solver_argument_codes():
     assert L.RK_MPI_SA_cleanup() == 0
     assert L.RK_MPI_SA_solve(1.0, C.byref(sysm)) == -3          # not initialised
     assert L.RK_MPI_SA_check_NAN() == 0
+    if P.device_count() == 0:
+        # with the arguments valid, the first device allocation fails: the added code -7
+        assert L.RK_MPI_SA_init(100, P.MPI_COMM_WORLD, 0) == 0
+        assert L.RK_MPI_SA_solve(1.0, C.byref(sysm)) == P.PFT_SOLVE_DEVICE_ERROR
+        assert L.pft_solver_last_status() <= -1000
+        assert L.RK_MPI_SA_cleanup() == 0
+    assert L.pft_solver_set_option(P.PFT_OPT_LAZY_ALLOC, 0) == 0
