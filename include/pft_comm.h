@@ -8,11 +8,21 @@
  *   - MPI_Allreduce(MAX) of eps (hybrid2.c:572) -> pft_comm_allreduce_eps (device buffer, RCCL);
  *   - MPI_Bcast of t/h/delta/... and of the command (hybrid2.c:328-336,616,690) -> pft_comm_bcast.
  *
- * One process per GPU: rank r drives GPU `device` and holds Z-slab r (rank 0 = bottom).
- * Transports: "self" (1 rank), "rccl" (one process per GPU, production), "loopback" (several
- * slabs in ONE process, one host thread per slab, device-to-device copies; used to exercise
- * the multi-slab path on a single GPU).  The communicator in use is per host thread
- * (pft_comm_set_current), as the reference solver's MPI state is per process.
+ * One process per slab: rank r drives GPU `device` and holds Z-slab r (rank 0 = bottom).
+ * Transports:
+ *   "ipc"      one process per slab on one node (one slab per GPU, or several on one GPU): the
+ *              neighbours' slab buffers are IPC-mapped (hipIpcOpenMemHandle, over xGMI between
+ *              GPUs), each stage's boundary planes are stored straight into the neighbours' ghost
+ *              planes by a put kernel that then raises their flag words, and each compute stream
+ *              waits for its own flags (hipStreamWaitValue64): one launch per stage, no collective
+ *              library, no host round trip.  The eps max and the broadcasts are host rounds over a
+ *              POSIX shared-memory segment.
+ *   "rccl"     one process per GPU, RCCL ncclSend/ncclRecv on a priority stream beside the
+ *              interior sweep (boundary planes launched first).
+ *   "loopback" several slabs in ONE process, one host thread per slab, device-to-device copies.
+ *   "self"     one rank.
+ * The communicator in use is per host thread (pft_comm_set_current), as the reference solver's
+ * MPI state is per process.
  */
 #ifndef PFT_COMM_H
 #define PFT_COMM_H
@@ -32,6 +42,10 @@ int pft_comm_init_self(pft_comm ** c);
    through torch.distributed's store) */
 int pft_comm_get_unique_id(void * id_bytes);
 int pft_comm_init_rccl(pft_comm ** c, int nranks, int rank, const void * id_bytes, int device);
+/* ipc: every rank passes the same POSIX shared-memory name ("/..."; rank 0 creates the segment
+   and unlinks the name once all ranks have mapped it) and its HIP device.  Peers are waited for
+   up to PFT_IPC_TIMEOUT seconds (environment, default 300); a timeout returns -5000. */
+int pft_comm_init_ipc(pft_comm ** c, int nranks, int rank, const char * name, int device);
 /* loopback: create once, then each of the nranks threads calls pft_comm_loopback_rank() */
 int pft_comm_init_loopback(pft_comm ** group, int nranks);
 int pft_comm_loopback_rank(pft_comm * group, int rank, pft_comm ** mine);
@@ -41,11 +55,14 @@ int pft_comm_rank(const pft_comm * c);
 /* 1 when the stage pipeline splits boundary planes from the interior and exchanges halos
    (more than one rank, or the self-exchange diagnostic) */
 int pft_comm_splits(const pft_comm * c);
-/* diagnostic, 1-rank RCCL communicator only: run the multi-rank stage pipeline on one GPU, the
-   halo exchange sending the slab's boundary planes to its own ghost planes (never read by a
-   single slab) and the eps max through ncclAllReduce -- the per-rank cost of the N > 1 path
-   without the xGMI transfer time (bench.py --self-exchange) */
+/* diagnostic, 1-rank RCCL or ipc communicator, before a slab is attached: run the multi-rank
+   stage pipeline on one GPU, the halo exchange sending the slab's boundary planes to its own
+   ghost planes (never read by a single slab) -- the per-rank cost of the N > 1 path without the
+   xGMI transfer time (bench.py --self-exchange) */
 int pft_comm_set_self_exchange(pft_comm * c, int on);
+/* 1: the ipc transport exchanges halos (more than one rank, or the self exchange): every stage is
+   one launch over all planes followed by the stream-ordered put + wait (no boundary split) */
+int pft_comm_device_halo(const pft_comm * c);
 int pft_comm_size(const pft_comm * c);
 const char * pft_comm_kind(const pft_comm * c);
 
@@ -68,8 +85,12 @@ int pft_comm_halo_finish(pft_comm * c);
    later work on the comm stream follows it in stream order */
 int pft_comm_halo_enqueue_comm(pft_comm * c, int buf, int f0, int f1);
 int pft_comm_halo(pft_comm * c, int buf, int f0, int f1);   /* start + finish */
-/* eps max over ranks, on the slab's scratch (u64 bits + non-finite flag), stream-ordered */
+/* eps max over ranks, on the slab's scratch (u64 bits + non-finite flag), stream-ordered
+   (rccl, loopback; a no-op for ipc, whose max is pft_comm_eps_host) */
 int pft_comm_allreduce_eps(pft_comm * c);
+/* ipc: the max over ranks of the error norm the host fetched (and the OR of the non-finite
+   flags), one shared-memory round; a no-op for the other transports */
+int pft_comm_eps_host(pft_comm * c, double * eps, int * nonfinite);
 /* eps max over ranks + its publication to pinned host memory (pft_slab_eps_mark): with RCCL both
    run on the communication stream, off the compute stream's critical path (the speculative
    stage 1 is enqueued right after); a single rank just publishes */

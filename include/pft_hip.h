@@ -180,6 +180,22 @@ int pft_h2d(void * dst, const void * src, size_t bytes, void * stream);
 /* diagnostic: plain 8-byte-per-lane device copy (rocprofv3 FETCH_SIZE/WRITE_SIZE calibration) */
 int pft_probe_copy(double * dst, const double * src, size_t n, void * stream);
 
+/* ipc transport (pft_comm.h).  Every rank swaps its buffers identically, so a buffer role names
+   the same physical allocation on every slab; the neighbours' allocations are mapped once.
+   export: the slab's PFT_BUF_COUNT buffer allocations + its flag words as PFT_BUF_COUNT + 1
+   hipIpcMemHandle_t (64 bytes each, PFT_IPC_HANDLE_BYTES in all);
+   set_peer(side 0 = below / 1 = above): open the neighbour's handles (handles = NULL: the slab
+   itself, the one-GPU self-exchange diagnostic); n3 / fs are the neighbour's planes and stride;
+   halo_put: boundary planes 1 and n3 of buffer `role`, fields [f0, f1), into the neighbours' ghost
+   planes, then `seq` into their flag words (one kernel on the compute stream);
+   halo_wait: the compute stream waits until both neighbours' flags reach `seq`. */
+#define PFT_IPC_HANDLE_BYTES (64 * (PFT_BUF_COUNT + 1))
+int pft_slab_ipc_export(pft_slab * s, void * handles);
+int pft_slab_ipc_set_peer(pft_slab * s, int side, const void * handles, int n3, long fs);
+int pft_slab_ipc_close(pft_slab * s);
+int pft_slab_halo_put(pft_slab * s, int role, int f0, int f1, unsigned long long seq);
+int pft_slab_halo_wait(pft_slab * s, unsigned long long seq);
+
 /* peer copy of one ghost plane between slabs on the same process (loopback transport) */
 int pft_memcpy_d2d_async(void * dst, const void * src, size_t bytes, void * stream);
 int pft_event_record_wait(void * from_stream, void * to_stream);

@@ -132,6 +132,8 @@ def lib():
         L.pft_comm_get_unique_id.argtypes = [C.c_void_p]
         L.pft_comm_init_rccl.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_void_p, C.c_int]
         L.pft_comm_init_loopback.argtypes = [C.POINTER(C.c_void_p), C.c_int]
+        L.pft_comm_init_ipc.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_char_p, C.c_int]
+        L.pft_comm_device_halo.argtypes = [C.c_void_p]
         L.pft_comm_loopback_rank.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
         L.pft_comm_set_current.argtypes = [C.c_void_p]
         L.pft_comm_destroy.argtypes = [C.c_void_p]
@@ -177,6 +179,22 @@ def decompose(total_n3, nprocs, rank):
     n3, fr = C.c_int(), C.c_int()
     lib().pft_decompose(total_n3, nprocs, rank, C.byref(n3), C.byref(fr))
     return n3.value, fr.value
+
+
+def comm_init_ipc(nranks, rank, name, device=0):
+    """the ipc communicator of rank `rank` (pft_comm.h): every rank passes the same shared-memory
+    name ("/..."), rank 0 creates it; bound to this thread (pft_comm_set_current).  Returns the handle."""
+    c = C.c_void_p()
+    rc = lib().pft_comm_init_ipc(C.byref(c), nranks, rank, name.encode(), device)
+    if rc:
+        raise RuntimeError(f"pft_comm_init_ipc(rank {rank}) failed ({rc}): {lib().pft_hip_last_error()}")
+    lib().pft_comm_set_current(c)
+    return c
+
+
+def comm_destroy(c):
+    lib().pft_comm_set_current(None)
+    lib().pft_comm_destroy(c)
 
 
 def params_array(values):

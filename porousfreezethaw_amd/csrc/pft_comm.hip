@@ -1,20 +1,57 @@
 // pft_comm.hip -- inter-slab communication for libpft (see include/pft_comm.h).
 //
 // Replaces the reference's MPI calls on the hot path (equation.c:290-326 sync_solution,
-// RK_MPI_SAsolver_hybrid2.c:572 eps Allreduce, :328-336/:616/:690 Bcasts).  Production transport:
-// RCCL (the librccl of /opt/rocm) with one process per GPU; every call is stream-ordered on the
-// slab's streams so the host never waits inside a stage.  Test transport: "loopback" -- several
-// slabs in one process (one host thread each), exchanging planes with device copies.
+// RK_MPI_SAsolver_hybrid2.c:572 eps Allreduce, :328-336/:616/:690 Bcasts).  Transports:
+//  - ipc: one process per slab on one node.  Each slab's buffers are mapped into its
+//    z-neighbours' processes (hipIpcOpenMemHandle; same GPU or a peer GPU over xGMI); a stage's
+//    boundary planes are stored straight into the neighbours' ghost planes by a put kernel that
+//    then raises their flag words, and each stream waits for its own flags
+//    (hipStreamWaitValue64).  Host-level collectives (the eps max, broadcasts) go through a POSIX
+//    shared-memory segment.  No collective library, no host round trip per stage.
+//  - rccl: the librccl of /opt/rocm, one process per GPU, ncclSend/ncclRecv on a priority stream.
+//  - loopback: several slabs in one process (one host thread each), device copies (tests).
+#include <errno.h>
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <pthread.h>
 #include <rccl/rccl.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
 
 #include "../../include/pft_comm.h"
 
-enum { KIND_SELF = 0, KIND_RCCL = 1, KIND_LOOP = 2 };
+enum { KIND_SELF = 0, KIND_RCCL = 1, KIND_LOOP = 2, KIND_IPC = 3 };
+
+// ---- ipc rendezvous segment ---------------------------------------------------------------
+#define PFT_IPC_MAX 64
+#define PFT_IPC_MAGIC 0x7066745f69706331ULL   // "pft_ipc1"
+
+struct IpcSlot {              // one rank's slab, published at attach
+  int n3;
+  long fs;
+  char handles[PFT_IPC_HANDLE_BYTES];
+};
+
+struct IpcRound {             // one rank's part of a host collective round
+  unsigned long long seq;     // written last (release): the round this payload belongs to
+  unsigned long long v[2];
+  long long iv;
+  char bytes[256];
+};
+
+struct IpcShared {
+  unsigned long long magic;
+  int nranks;
+  IpcSlot slot[PFT_IPC_MAX];
+  IpcRound round[2][PFT_IPC_MAX];   // by round parity: round n+2 may reuse round n's records
+                                    // only once every rank has posted round n+1
+};
 
 struct LoopGroup {
   int n;
@@ -36,10 +73,65 @@ struct pft_comm {
   hipEvent_t ev_ready, ev_done;
   int pending;
   void* dscratch;   // 256 bytes of device memory for host-level collectives
-  int self_x;       // diagnostic: 1-rank RCCL communicator exchanging with itself
+  int self_x;       // diagnostic: 1-rank communicator exchanging with itself
+  // ipc
+  IpcShared* shm;
+  char shm_name[128];
+  unsigned long long hseq;   // host collective rounds so far (identical on every rank)
+  unsigned long long dseq;   // device halo exchanges so far (identical on every rank)
+  double timeout_s;
+  void* bcast_pinned;        // rccl: pinned host staging of pft_comm_bcast
 };
 
 static __thread pft_comm* g_current = nullptr;
+
+static double now_s()
+{
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+// spin on a shared-memory word (tight for ~50 us, then yielding), up to c->timeout_s
+static int ipc_wait_ge(const pft_comm* c, const unsigned long long* w, unsigned long long v)
+{
+  if (__atomic_load_n(w, __ATOMIC_ACQUIRE) >= v) return 0;
+  const double t0 = now_s();
+  for (long it = 0;; ++it) {
+    if (__atomic_load_n(w, __ATOMIC_ACQUIRE) >= v) return 0;
+    if (it < 20000) {
+      __builtin_ia32_pause();
+    } else {
+      sched_yield();
+      if ((it & 1023) == 0 && now_s() - t0 > c->timeout_s) {
+        fprintf(stderr, "pft_comm(ipc): rank %d timed out waiting for a peer (%.0f s)\n", c->rank, c->timeout_s);
+        return -5000;
+      }
+    }
+  }
+}
+
+// one host collective round: post this rank's payload, wait for every rank's; returns the records
+static int ipc_round(pft_comm* c, const unsigned long long v[2], long long iv, const void* bytes, int nbytes,
+                     IpcRound** recs)
+{
+  const unsigned long long seq = ++c->hseq;
+  IpcRound* R = c->shm->round[seq & 1];
+  IpcRound* me = &R[c->rank];
+  if (v) {
+    me->v[0] = v[0];
+    me->v[1] = v[1];
+  }
+  me->iv = iv;
+  if (bytes && nbytes > 0) memcpy(me->bytes, bytes, nbytes);
+  __atomic_store_n(&me->seq, seq, __ATOMIC_RELEASE);
+  for (int q = 0; q < c->size; ++q) {
+    const int rc = ipc_wait_ge(c, &R[q].seq, seq);
+    if (rc) return rc;
+  }
+  *recs = R;
+  return 0;
+}
 
 #define NCCLCHK(x)                                                         \
   do {                                                                     \
@@ -103,6 +195,80 @@ int pft_comm_init_rccl(pft_comm** c, int nranks, int rank, const void* id_bytes,
   return 0;
 }
 
+int pft_comm_init_ipc(pft_comm** c, int nranks, int rank, const char* name, int device)
+{
+  *c = nullptr;
+  if (nranks < 1 || nranks > PFT_IPC_MAX || rank < 0 || rank >= nranks || !name || name[0] != '/' ||
+      strlen(name) >= 128)
+    return -2;
+  HCHK(hipSetDevice(device));
+  pft_comm* m = (pft_comm*)calloc(1, sizeof(pft_comm));
+  m->kind = KIND_IPC;
+  m->rank = rank;
+  m->size = nranks;
+  m->device = device;
+  const char* to = getenv("PFT_IPC_TIMEOUT");
+  m->timeout_s = to ? atof(to) : 300.0;
+  snprintf(m->shm_name, sizeof(m->shm_name), "%s", name);
+  const size_t bytes = sizeof(IpcShared);
+  int fd = -1;
+  const double t0 = now_s();
+  if (rank == 0) {
+    fd = shm_open(name, O_RDWR | O_CREAT | O_EXCL, 0600);
+    if (fd >= 0 && ftruncate(fd, (off_t)bytes) != 0) {
+      close(fd);
+      fd = -1;
+    }
+  } else {
+    // wait for rank 0 to create and size the segment
+    while (true) {
+      fd = shm_open(name, O_RDWR, 0600);
+      if (fd >= 0) {
+        struct stat st;
+        if (fstat(fd, &st) == 0 && (size_t)st.st_size == bytes) break;
+        close(fd);
+        fd = -1;
+      }
+      if (now_s() - t0 > m->timeout_s) break;
+      usleep(1000);
+    }
+  }
+  if (fd < 0) {
+    fprintf(stderr, "pft_comm(ipc): rank %d: shared memory %s: %s\n", rank, name, strerror(errno));
+    free(m);
+    return -5001;
+  }
+  void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) {
+    free(m);
+    return -5001;
+  }
+  m->shm = (IpcShared*)p;
+  if (rank == 0) {
+    m->shm->nranks = nranks;
+    __atomic_store_n(&m->shm->magic, PFT_IPC_MAGIC, __ATOMIC_RELEASE);
+  } else {
+    int rc = ipc_wait_ge(m, &m->shm->magic, PFT_IPC_MAGIC);
+    if (rc || m->shm->nranks != nranks) {
+      munmap(p, bytes);
+      free(m);
+      return rc ? rc : -2;
+    }
+  }
+  // everyone is mapped: rank 0 may unlink the name (the mappings stay), so nothing is left behind
+  IpcRound* recs;
+  int rc = ipc_round(m, nullptr, 0, nullptr, 0, &recs);
+  if (rank == 0) shm_unlink(name);
+  if (rc) {
+    munmap(p, bytes);
+    free(m);
+    return rc;
+  }
+  *c = m;
+  return 0;
+}
+
 int pft_comm_init_loopback(pft_comm** group, int nranks)
 {
   if (nranks < 1) return -2;
@@ -144,6 +310,11 @@ int pft_comm_destroy(pft_comm* c)
     (void)hipEventDestroy(c->ev_done);
     (void)hipFree(c->dscratch);
   }
+  if (c->kind == KIND_IPC) {
+    if (c->slab) pft_comm_attach(c, nullptr);
+    munmap(c->shm, sizeof(IpcShared));
+  }
+  if (c->bcast_pinned) (void)hipHostFree(c->bcast_pinned);
   if (c->kind == KIND_LOOP && c->rank < 0) {
     pthread_barrier_destroy(&c->grp->bar);
     free(c->grp->slabs);
@@ -159,15 +330,16 @@ int pft_comm_rank(const pft_comm* c) { return c ? c->rank : 0; }
 int pft_comm_splits(const pft_comm* c) { return c && (c->size > 1 || c->self_x); }
 int pft_comm_set_self_exchange(pft_comm* c, int on)
 {
-  if (!c || c->kind != KIND_RCCL || c->size != 1) return -2;
+  if (!c || (c->kind != KIND_RCCL && c->kind != KIND_IPC) || c->size != 1 || c->slab) return -2;
   c->self_x = on ? 1 : 0;
   return 0;
 }
+int pft_comm_device_halo(const pft_comm* c) { return c && c->kind == KIND_IPC && (c->size > 1 || c->self_x); }
 int pft_comm_size(const pft_comm* c) { return c ? c->size : 1; }
 const char* pft_comm_kind(const pft_comm* c)
 {
   if (!c || c->kind == KIND_SELF) return "self";
-  return c->kind == KIND_RCCL ? "rccl" : "loopback";
+  return c->kind == KIND_RCCL ? "rccl" : c->kind == KIND_IPC ? "ipc" : "loopback";
 }
 
 int pft_comm_set_current(pft_comm* c)
@@ -177,9 +349,47 @@ int pft_comm_set_current(pft_comm* c)
 }
 pft_comm* pft_comm_current(void) { return g_current; }
 
+static int ipc_attach(pft_comm* c, pft_slab* s)
+{
+  // collective: every rank attaches / detaches its slab at the same point of the run
+  IpcRound* recs;
+  int rc;
+  if (c->slab) {
+    // nobody may still write into the buffers about to be unmapped (or freed)
+    HCHK(hipStreamSynchronize((hipStream_t)pft_slab_stream(c->slab)));
+    if ((rc = ipc_round(c, nullptr, 0, nullptr, 0, &recs))) return rc;
+    pft_slab_ipc_close(c->slab);
+    c->slab = nullptr;
+  }
+  if (!s) return 0;
+  IpcSlot* me = &c->shm->slot[c->rank];
+  if ((rc = pft_slab_ipc_export(s, me->handles))) return rc;
+  me->n3 = pft_slab_nz(s);
+  me->fs = (long)pft_slab_field_stride(s);
+  if ((rc = ipc_round(c, nullptr, 0, nullptr, 0, &recs))) return rc;   // every slot is published
+  if (c->self_x) {
+    if ((rc = pft_slab_ipc_set_peer(s, 0, nullptr, 0, 0)) || (rc = pft_slab_ipc_set_peer(s, 1, nullptr, 0, 0)))
+      return rc;
+  } else {
+    if (c->rank > 0) {
+      const IpcSlot* b = &c->shm->slot[c->rank - 1];
+      if ((rc = pft_slab_ipc_set_peer(s, 0, b->handles, b->n3, b->fs))) return rc;
+    }
+    if (c->rank < c->size - 1) {
+      const IpcSlot* a = &c->shm->slot[c->rank + 1];
+      if ((rc = pft_slab_ipc_set_peer(s, 1, a->handles, a->n3, a->fs))) return rc;
+    }
+  }
+  // the slots are reused by the next attach only after everyone has read them
+  if ((rc = ipc_round(c, nullptr, 0, nullptr, 0, &recs))) return rc;
+  c->slab = s;
+  return 0;
+}
+
 int pft_comm_attach(pft_comm* c, pft_slab* s)
 {
   if (!c) return -2;
+  if (c->kind == KIND_IPC) return c->slab == s ? 0 : ipc_attach(c, s);
   c->slab = s;
   if (c->kind == KIND_LOOP) c->grp->slabs[c->rank] = s;
   return 0;
@@ -202,6 +412,13 @@ static int halo_start(pft_comm* c, int buf, int f0, int f1, bool on_comm)
   // self exchange (diagnostic, one slab): the boundary planes go to the slab's own ghost planes,
   // which a single slab never reads (mirror bottom wall, Dirichlet top)
   const int pb = c->self_x ? c->rank : c->rank - 1, pa = c->self_x ? c->rank : c->rank + 1;
+  if (c->kind == KIND_IPC) {
+    // stream-ordered on the compute stream: put (boundary planes into the neighbours' ghost
+    // planes, then their flags), then wait for our own flags
+    const unsigned long long seq = ++c->dseq;
+    int rc = pft_slab_halo_put(s, buf, f0, f1, seq);
+    return rc ? rc : pft_slab_halo_wait(s, seq);
+  }
   if (c->kind == KIND_RCCL) {
     hipStream_t cs = (hipStream_t)pft_slab_comm_stream(s);
     if (!on_comm) {
@@ -268,7 +485,7 @@ int pft_comm_halo(pft_comm* c, int buf, int f0, int f1)
 
 int pft_comm_allreduce_eps(pft_comm* c)
 {
-  if (!pft_comm_splits(c)) return 0;
+  if (!pft_comm_splits(c) || c->kind == KIND_IPC) return 0;   // ipc: pft_comm_eps_host
   pft_slab* s = c->slab;
   hipStream_t st = (hipStream_t)pft_slab_stream(s);
   unsigned long long* d = (unsigned long long*)pft_slab_scratch(s);
@@ -300,7 +517,7 @@ int pft_comm_eps_publish(pft_comm* c)
 {
   if (!c || !c->slab) return -2;
   pft_slab* s = c->slab;
-  if (!pft_comm_splits(c)) return pft_slab_eps_mark(s);
+  if (!pft_comm_splits(c) || c->kind == KIND_IPC) return pft_slab_eps_mark(s);   // ipc: pft_comm_eps_host
   if (c->kind == KIND_RCCL) {
     // the max over ranks and the publication run on the communication stream, so the compute
     // stream goes on with the speculative stage 1 while RCCL reduces
@@ -318,16 +535,48 @@ int pft_comm_eps_publish(pft_comm* c)
   return rc ? rc : pft_slab_eps_mark(s);
 }
 
+int pft_comm_eps_host(pft_comm* c, double* eps, int* nonfinite)
+{
+  if (!c || c->kind != KIND_IPC || c->size == 1) return 0;
+  // max of non-negative doubles == max of their bit patterns; the non-finite flag: any rank's
+  unsigned long long v[2];
+  memcpy(&v[0], eps, 8);
+  v[1] = (unsigned long long)(nonfinite && *nonfinite);
+  IpcRound* R;
+  int rc = ipc_round(c, v, 0, nullptr, 0, &R);
+  if (rc) return rc;
+  unsigned long long m0 = 0, m1 = 0;
+  for (int q = 0; q < c->size; ++q) {
+    if (R[q].v[0] > m0) m0 = R[q].v[0];
+    m1 |= R[q].v[1];
+  }
+  memcpy(eps, &m0, 8);
+  if (nonfinite) *nonfinite = (int)(m1 != 0);
+  return 0;
+}
+
 int pft_comm_bcast(pft_comm* c, void* data, int bytes, int root)
 {
   if (!c || c->size == 1) return 0;
   if (bytes > 256) return -2;
+  if (c->kind == KIND_IPC) {
+    IpcRound* R;
+    int rc = ipc_round(c, nullptr, 0, c->rank == root ? data : nullptr, bytes, &R);
+    if (!rc && c->rank != root) memcpy(data, R[root].bytes, bytes);
+    return rc;
+  }
   if (c->kind == KIND_RCCL) {
-    hipStream_t st = c->slab ? (hipStream_t)pft_slab_stream(c->slab) : 0;
-    HCHK(hipMemcpyAsync(c->dscratch, data, bytes, hipMemcpyHostToDevice, st));
+    // on the communication stream through pinned host memory: the host waits for that stream
+    // only -- not for the compute stream's speculative stage 1 (the comm stream holds at most the
+    // boundary planes' exchange of it)
+    hipStream_t st = c->slab ? (hipStream_t)pft_slab_comm_stream(c->slab) : 0;
+    if (!c->bcast_pinned) HCHK(hipHostMalloc(&c->bcast_pinned, 256, hipHostMallocDefault));
+    memcpy(c->bcast_pinned, data, bytes);
+    HCHK(hipMemcpyAsync(c->dscratch, c->bcast_pinned, bytes, hipMemcpyHostToDevice, st));
     NCCLCHK(ncclBroadcast(c->dscratch, c->dscratch, bytes, ncclUint8, root, c->nccl, st));
-    HCHK(hipMemcpyAsync(data, c->dscratch, bytes, hipMemcpyDeviceToHost, st));
+    HCHK(hipMemcpyAsync(c->bcast_pinned, c->dscratch, bytes, hipMemcpyDeviceToHost, st));
     HCHK(hipStreamSynchronize(st));
+    memcpy(data, c->bcast_pinned, bytes);
     return 0;
   }
   if (c->rank == root) memcpy(c->grp->bbuf, data, bytes);
@@ -340,6 +589,16 @@ int pft_comm_bcast(pft_comm* c, void* data, int bytes, int root)
 int pft_comm_allreduce_max_i64(pft_comm* c, long long* v)
 {
   if (!c || c->size == 1) return 0;
+  if (c->kind == KIND_IPC) {
+    IpcRound* R;
+    int rc = ipc_round(c, nullptr, *v, nullptr, 0, &R);
+    if (rc) return rc;
+    long long m = R[0].iv;
+    for (int q = 1; q < c->size; ++q)
+      if (R[q].iv > m) m = R[q].iv;
+    *v = m;
+    return 0;
+  }
   if (c->kind == KIND_RCCL) {
     hipStream_t st = c->slab ? (hipStream_t)pft_slab_stream(c->slab) : 0;
     HCHK(hipMemcpyAsync(c->dscratch, v, 8, hipMemcpyHostToDevice, st));

@@ -1159,6 +1159,52 @@ __global__ void flat_combine_kernel(int stage, int n_chunks, const int* __restri
 }
 
 // ------------------------------------------------------------------------------------------
+// ipc transport (pft_comm.h): this slab's boundary planes go straight into the z-neighbours' ghost
+// planes (IPC-mapped device memory, on this GPU or over xGMI), then the last workgroup publishes the
+// exchange's sequence number in the neighbours' flag words; each side's stream waits for its own
+// flags (hipStreamWaitValue64), so the next stage starts only once both ghost planes are in.
+
+struct PutArgs {
+  const double* src;          // this slab's buffer (one role)
+  long fs;
+  int plane, n3, f0, nf;
+  double* dlo;                // the neighbour below: its top ghost plane (n3' + 1) of field 0, or null
+  long dlo_fs;
+  double* dhi;                // the neighbour above: its bottom ghost plane (0) of field 0, or null
+  long dhi_fs;
+  unsigned long long* slo;    // the neighbour below's flag "from above"
+  unsigned long long* shi;    // the neighbour above's flag "from below"
+  unsigned int* count;        // workgroups done (this slab's own memory)
+  unsigned long long seq;
+};
+
+__global__ __launch_bounds__(256) void halo_put_kernel(PutArgs a)
+{
+  const long n = (long)a.nf * a.plane;   // doubles per side
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < 2 * n; e += (long)gridDim.x * blockDim.x) {
+    const bool up = e >= n;
+    const long r = up ? e - n : e;
+    const int f = (int)(r / a.plane);
+    const long c = r - (long)f * a.plane;
+    if (!up) {
+      if (a.dlo) a.dlo[(a.f0 + f) * a.dlo_fs + c] = a.src[(a.f0 + f) * a.fs + (long)a.plane + c];       // plane 1
+    } else {
+      if (a.dhi) a.dhi[(a.f0 + f) * a.dhi_fs + c] = a.src[(a.f0 + f) * a.fs + (long)a.n3 * a.plane + c];  // plane n3
+    }
+  }
+  // every workgroup's stores are visible system-wide before it is counted; the last one counted
+  // raises the flags (release), so a neighbour that sees the flag sees the whole plane
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(a.count, 1u) == gridDim.x - 1) {
+    atomicExch(a.count, 0u);
+    __threadfence_system();
+    if (a.slo) __hip_atomic_store(a.slo, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (a.shi) __hip_atomic_store(a.shi, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // calibration probe: a plain 8-byte-per-lane copy with a known byte count, used to calibrate
 // rocprofv3's FETCH_SIZE / WRITE_SIZE for the access width the stage kernels use
 
@@ -1171,12 +1217,29 @@ __global__ void probe_copy_kernel(double* __restrict__ dst, const double* __rest
 // ------------------------------------------------------------------------------------------
 // slab object + shim
 
+// a z-neighbour's buffers mapped into this process (ipc transport): the put kernel and the fused
+// stage kernels store this slab's boundary planes straight into the neighbour's ghost plane
+struct SlabPeer {
+  int on;                              // 1: a neighbour on this side receives our boundary planes
+  int opened;                          // 1: base[] / sig came from hipIpcOpenMemHandle (close them)
+  double* base[PFT_BUF_COUNT];         // the neighbour's buffers by physical index
+  unsigned long long* sig;             // the neighbour's flag words
+  long fs;                             // its field stride
+  int n3;                              // its interior planes
+};
+
 struct pft_slab {
   pft_slab_desc d;
   pft_consts c;
   long fs;
   int plane;
   double* buf[PFT_BUF_COUNT];
+  double* buf0[PFT_BUF_COUNT];   // the allocations by physical index (buf[] is permuted by swaps)
+  int phys[PFT_BUF_COUNT];       // role -> physical index; every rank swaps identically, so a role
+                                 // names the same physical buffer on every slab
+  unsigned long long* sig;       // flag words written by the neighbours: [0] from below, [1] from
+                                 // above (monotonic exchange sequence numbers); [8] put counter
+  SlabPeer peer[2];              // [0] the neighbour below, [1] above
   double* staging;       // host padded layout on the device (for upload/download)
   long S;                // host padded block (one field)
   unsigned long long* scratch;  // [0] eps bits, [1] nonfinite flag
@@ -1267,8 +1330,12 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
   if (e == hipSuccess) e = hipHostMalloc((void**)&s->host_scratch, 64, hipHostMallocDefault);
   if (e == hipSuccess) e = hipHostMalloc((void**)&s->host_pub, 64, hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&s->host_pub_dev, s->host_pub, 0);
+  if (e == hipSuccess) e = hipMalloc((void**)&s->sig, 4096);
+  if (e == hipSuccess) e = hipMemsetAsync(s->sig, 0, 4096, s->stream);
   for (int b = 0; b < PFT_BUF_COUNT && e == hipSuccess; ++b) {
     e = hipMalloc((void**)&s->buf[b], bytes);
+    s->buf0[b] = s->buf[b];
+    s->phys[b] = b;
     // zero-fill on the slab's own stream: the compute stream is non-blocking, so a fill on the
     // null stream would not be ordered before the first upload/kernel (it raced with them)
     if (e == hipSuccess) e = hipMemsetAsync(s->buf[b], 0, bytes, s->stream);
@@ -1288,8 +1355,10 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
 int pft_slab_destroy(pft_slab* s)
 {
   if (!s) return 0;
+  (void)pft_slab_ipc_close(s);
   for (int b = 0; b < PFT_BUF_COUNT; ++b)
-    if (s->buf[b]) (void)hipFree(s->buf[b]);
+    if (s->buf0[b]) (void)hipFree(s->buf0[b]);
+  if (s->sig) (void)hipFree(s->sig);
   if (s->staging) (void)hipFree(s->staging);
   if (s->noise) (void)hipFree(s->noise);
   for (int st = 0; st < 6; ++st)
@@ -1878,14 +1947,106 @@ int pft_slab_swap_buffers(pft_slab* s, int a, int b)
   double* t = s->buf[a];
   s->buf[a] = s->buf[b];
   s->buf[b] = t;
+  const int p = s->phys[a];
+  s->phys[a] = s->phys[b];
+  s->phys[b] = p;
   return 0;
 }
 
-int pft_slab_accept(pft_slab* s)
+int pft_slab_accept(pft_slab* s) { return pft_slab_swap_buffers(s, PFT_BUF_X, PFT_BUF_XN); }
+
+int pft_slab_ipc_export(pft_slab* s, void* handles)
 {
-  double* t = s->buf[PFT_BUF_X];
-  s->buf[PFT_BUF_X] = s->buf[PFT_BUF_XN];
-  s->buf[PFT_BUF_XN] = t;
+  hipIpcMemHandle_t* h = (hipIpcMemHandle_t*)handles;
+  for (int b = 0; b < PFT_BUF_COUNT; ++b) HIPCHK(hipIpcGetMemHandle(&h[b], s->buf0[b]));
+  HIPCHK(hipIpcGetMemHandle(&h[PFT_BUF_COUNT], s->sig));
+  return 0;
+}
+
+int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, long fs)
+{
+  if (side < 0 || side > 1) return -2;
+  SlabPeer& p = s->peer[side];
+  if (p.on) return -2;                  // pft_slab_ipc_close first
+  if (!handles) {
+    // self exchange (diagnostic, one slab): the planes land in the slab's own ghost planes, which a
+    // single slab never reads (mirror bottom, Dirichlet top)
+    for (int b = 0; b < PFT_BUF_COUNT; ++b) p.base[b] = s->buf0[b];
+    p.sig = s->sig;
+    p.n3 = s->d.n3;
+    p.fs = s->fs;
+    p.opened = 0;
+    p.on = 1;
+    return 0;
+  }
+  const hipIpcMemHandle_t* h = (const hipIpcMemHandle_t*)handles;
+  for (int b = 0; b <= PFT_BUF_COUNT; ++b) {
+    void* ptr = nullptr;
+    const hipError_t e = hipIpcOpenMemHandle(&ptr, h[b], hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+      for (int q = 0; q < b; ++q) (void)hipIpcCloseMemHandle(p.base[q]);
+      return fail(e, "hipIpcOpenMemHandle");
+    }
+    if (b < PFT_BUF_COUNT) p.base[b] = (double*)ptr;
+    else p.sig = (unsigned long long*)ptr;
+  }
+  p.n3 = n3;
+  p.fs = fs;
+  p.opened = 1;
+  p.on = 1;
+  return 0;
+}
+
+int pft_slab_ipc_close(pft_slab* s)
+{
+  for (int side = 0; side < 2; ++side) {
+    SlabPeer& p = s->peer[side];
+    if (p.on && p.opened) {
+      for (int b = 0; b < PFT_BUF_COUNT; ++b) (void)hipIpcCloseMemHandle(p.base[b]);
+      (void)hipIpcCloseMemHandle(p.sig);
+    }
+    memset(&p, 0, sizeof(p));
+  }
+  return 0;
+}
+
+int pft_slab_halo_put(pft_slab* s, int role, int f0, int f1, unsigned long long seq)
+{
+  if (role < 0 || role >= PFT_BUF_COUNT || f0 < 0 || f1 > 3 || f1 <= f0) return -2;
+  const int ph = s->phys[role];
+  PutArgs a;
+  memset(&a, 0, sizeof(a));
+  a.src = s->buf[role];
+  a.fs = s->fs;
+  a.plane = s->plane;
+  a.n3 = s->d.n3;
+  a.f0 = f0;
+  a.nf = f1 - f0;
+  if (s->peer[0].on) {
+    a.dlo = s->peer[0].base[ph] + (long)(s->peer[0].n3 + 1) * s->plane;
+    a.dlo_fs = s->peer[0].fs;
+    a.slo = s->peer[0].sig + 1;
+  }
+  if (s->peer[1].on) {
+    a.dhi = s->peer[1].base[ph];
+    a.dhi_fs = s->peer[1].fs;
+    a.shi = s->peer[1].sig + 0;
+  }
+  if (!a.slo && !a.shi) return 0;
+  a.count = (unsigned int*)(s->sig + 8);
+  a.seq = seq;
+  const long n = 2L * a.nf * s->plane;
+  const int blocks = (int)std::min<long>(1024, std::max<long>(1, (n + 255) / 256));
+  halo_put_kernel<<<blocks, 256, 0, s->stream>>>(a);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int pft_slab_halo_wait(pft_slab* s, unsigned long long seq)
+{
+  // flags [0] (from below) and [1] (from above): the stream goes on once both planes are in
+  for (int side = 0; side < 2; ++side)
+    if (s->peer[side].on) HIPCHK(hipStreamWaitValue64(s->stream, s->sig + side, seq, hipStreamWaitValueGte, ~0ULL));
   return 0;
 }
 

@@ -244,6 +244,14 @@ static int do_stage(int stage, double ts, double coef, double h, long * launches
 	const int tstage = stage == 6 ? 1 : stage;
 	int rc, n3;
 	if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 0);
+	if(pft_comm_device_halo(c)) {
+		/* ipc: the whole slab in one launch, then (stream-ordered) the boundary planes into the
+		   neighbours' ghost planes and the wait for theirs in ours */
+		(*launches)++;
+		if((rc = run1(stage, ts, coef, h, -1, -1))) return rc;
+		if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
+		return pft_comm_halo(c, out_buf, 0, nfields);
+	}
 	if(!pft_comm_splits(c)) {
 		(*launches)++;
 		rc = run1(stage, ts, coef, h, -1, -1);
@@ -424,6 +432,7 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 			if((rc = pft_comm_allreduce_eps(c))) return rc;                      /* :572 */
 		}
 		if((rc = pft_slab_eps_fetch(R.slab, &eps, &nonfinite))) return rc;
+		if((rc = pft_comm_eps_host(c, &eps, &nonfinite))) return rc;                 /* :572 (ipc) */
 		if(R.opt_timing) pft_slab_timing_collect(R.slab, R.stats.stage_ms, R.stats.stage_n);
 		system->steps_total++;                                                   /* :460 */
 		attempted++;

@@ -1,0 +1,117 @@
+"""The N > 1 path between separate processes: the ipc transport (pft_comm.h) with one process per
+Z-slab, all on one GPU here (the same code maps a neighbour on another GPU over xGMI).  Each rank
+is its own Python process started before it touches the GPU (tests/_ipc_worker.py); the slabs
+exchange boundary planes through IPC-mapped device memory and flag words, the eps max and the
+broadcasts through a shared-memory segment -- the reference's sync_solution (equation.c:290-326),
+MPI_Allreduce of eps (RK_MPI_SAsolver_hybrid2.c:572) and command broadcasts (:328-336, :690).
+
+Checked bit for bit (results do not depend on the decomposition):
+  - golden g20 (the reference's own trajectory, 1171 attempted steps to t = 720 s) on 2, 3 and 4
+    processes, default and fused-tile kernels;
+  - BASELINE's 400^3 split over 2 and 4 processes against the single-slab run, 12 attempted steps;
+  - the one-process ipc self exchange (the per-rank rehearsal of bench.py --self-exchange)."""
+import json
+import os
+import subprocess
+import sys
+import uuid
+
+import numpy as np
+import pytest
+
+import _multi as M
+import _oracle as O
+import porousfreezethaw_amd as P
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if P.device_count() < 1:
+        pytest.fail("no HIP device: the gpu tests must run on an MI355X (no CPU fallback exists)")
+
+
+def _run_ranks(tmp_path, nranks, timeout=240, **spec):
+    spec = dict(spec, nranks=nranks, shm=f"/pft_test_{os.getpid()}_{uuid.uuid4().hex[:12]}",
+                out=str(tmp_path / "rank"))
+    path = tmp_path / "spec.json"
+    path.write_text(json.dumps(spec))
+    env = dict(os.environ, PFT_IPC_TIMEOUT="120")
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "_ipc_worker.py"), str(path), str(r)],
+                              env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(nranks)]
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=timeout)
+            outs.append(out.decode(errors="replace"))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} failed ({p.returncode}):\n{outs[r][-3000:]}"
+    return [dict(np.load(f"{spec['out']}.{r}.npz")) for r in range(nranks)]
+
+
+@pytest.mark.parametrize("nranks,tile", [(2, None), (3, 32), (4, None), (4, 32)])
+def test_g20_processes_equal_reference(tmp_path, nranks, tile):
+    meta, A = O.load_case("g20")
+    times = meta["traj_times"]
+    res = _run_ranks(tmp_path, nranks, case="g20", times=times, tile=tile)
+    for r in res:
+        assert int(r["path"]) == 1
+    for i in range(len(times)):
+        ref = meta["traj_m0"][i]
+        for r in res:
+            t, h, s, st, rc = r["rows"][i]
+            assert (t.hex(), h.hex(), int(s), int(st), int(rc)) == \
+                (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(), ref[2], ref[3], ref[4])
+        full = np.concatenate([r["states"][i] for r in res], axis=1)
+        assert np.array_equal(full, A[f"traj_m0_state{i}"])
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_400_processes_equal_one_slab(tmp_path, nranks):
+    steps = 12
+    base, Pm, info = M.full_size_case(400, 0)
+    sim = P.Simulation(info["n1"], info["n2"], info["n3"], (info["L1"], info["L2"], info["L3"]), 0, Pm,
+                       beads=O.beads(), tau=1.0, tau_min=info["tau_min"], delta=info["delta"])
+    assert sim.solve_ex(1e9, steps, 0) == 2
+    got = (sim.t, sim.h, sim.system.steps, sim.system.steps_total)
+    x = sim.interior()
+    sim.close()
+    assert got[2] < got[3]                                    # a rejected step in the window
+    res = _run_ranks(tmp_path, nranks, case="default", grid_nodes=400, times=[1e9], steps=steps)
+    for r in res:
+        t, h, s, st, rc = r["rows"][0]
+        assert (t, h, int(s), int(st), int(rc)) == got + (2,)
+    assert [int(r["n3"]) for r in res] == [400 // nranks] * nranks
+    assert np.array_equal(np.concatenate([r["states"][0] for r in res], axis=1), x)
+
+
+@pytest.mark.parametrize("tile", [None, 32])
+def test_ipc_self_exchange_equals_reference(tile):
+    """one process, ipc communicator of size 1 exchanging with itself: the put kernel, the flag
+    words and the stream waits of every stage run; the planes land in ghost planes one slab never
+    reads, so the trajectory is the reference's"""
+    meta, A = O.load_case("g20")
+    Pm, info = O.params_from_meta(meta)
+    comm = P.comm_init_ipc(1, 0, f"/pft_selfx_{os.getpid()}_{uuid.uuid4().hex[:12]}")
+    try:
+        assert P.lib().pft_comm_set_self_exchange(comm, 1) == 0
+        assert P.lib().pft_comm_device_halo(comm) == 1
+        sim = P.Simulation(info["n1"], info["n2"], info["n3"], (info["L1"], info["L2"], info["L3"]), 0, Pm,
+                           initial=A["traj_m0_ic"], tau=1.0, tau_min=info["tau_min"], delta=info["delta"],
+                           tile=tile)
+        for i, T in enumerate(meta["traj_times"][:2]):
+            rc = sim.solve(T)
+            ref = meta["traj_m0"][i]
+            assert (sim.t.hex(), sim.h.hex(), sim.system.steps, sim.system.steps_total, rc) == \
+                (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(), ref[2], ref[3], ref[4])
+            assert np.array_equal(sim.interior(), A[f"traj_m0_state{i}"])
+        sim.close()
+    finally:
+        P.comm_destroy(comm)
