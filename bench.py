@@ -50,7 +50,6 @@ STAGE_DOUBLES_AUX = {False: {1: 9, 2: 12, 3: 15, 4: 18, 5: 18}, True: {1: 7, 2: 
 # stage 2 stores S = K1 + K2, so stage 3 reads x and S (PFT_K12_SUM); stage 5 stores gl's x(t+h)
 # only when it is not x itself (pft_slab_get_gl_keep: 11 doubles then, as with gl_static)
 STAGE_DOUBLES_RC = {False: {1: 5, 2: 7, 3: 7, 4: 9, 5: 12}, True: {1: 5, 2: 7, 3: 7, 4: 9, 5: 11}}
-SURVEY_BYTES_PER_CELL_STEP = 840   # unfused solver/RHS boundary accounting
 METRIC = "Mcells·RK-steps/s at 400³ grid, 1/2/4/8 MI355X; % HBM roofline"
 PUBLISHED_400_MODE1 = 351.88      # BASELINE.md 1, CC-HR-12nodes SigmaP1-P-smallsigma, 384 cores
 
@@ -82,10 +81,20 @@ def parse():
     ap.add_argument("--host-boundary", action="store_true",
                     help="timed call is one RK_MPI_SA_solve-style call: x copied host->device at entry "
                          "and back at exit (PCIe-inclusive rate; never the headline value)")
+    ap.add_argument("--transport", choices=("ipc", "rccl"), default="ipc",
+                    help="N>1 (and --self-exchange) inter-slab transport (pft_comm.h): ipc = IPC-mapped "
+                         "neighbour slabs, boundary planes stored into their ghost planes + flag words "
+                         "(default); rccl = ncclSend/ncclRecv on a priority stream beside the interior sweep")
     ap.add_argument("--self-exchange", action="store_true",
-                    help="diagnostic, 1 GPU: run the N>1 stage pipeline (boundary planes first, RCCL halo "
-                         "exchange on the comm stream beside the interior sweep, RCCL eps max) with a "
-                         "1-rank communicator exchanging with itself; never the headline value")
+                    help="diagnostic, 1 GPU: run the N>1 path of --transport (ipc: put kernel + flag waits "
+                         "per stage; rccl: boundary planes first, halo exchange beside the interior sweep, "
+                         "RCCL eps max) with a 1-rank communicator exchanging with itself; never the headline")
+    ap.add_argument("--callback", action="store_true",
+                    help="install a Service_Callback that reads t and h after every accepted step, as the "
+                         "reference driver's RKService does with its default Params (intertrack.c:1072-1116)")
+    ap.add_argument("--timing-steps", type=int, default=30,
+                    help="attempted steps of the separate, untimed pass that measures the stage kernels with "
+                         "HIP events (roofline); 0 = none")
     ap.add_argument("--two-stream", action="store_true",
                     help="N>1 stage pipeline on two streams (boundary launch and exchange on the comm stream "
                          "beside the interior sweep) instead of the default one-stream pipeline")
@@ -125,31 +134,15 @@ def main():
     comm = None
     if world > 1:
         # torch.distributed (gloo, host only) is the rendezvous and the barrier; the data path is
-        # libpft's RCCL communicator (pft_comm.h).  torch never touches the GPU here.
+        # libpft's communicator (pft_comm.h).  torch never touches the GPU here.
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        uid = (C.c_char * 128)()
-        if rank == 0:
-            assert L.pft_comm_get_unique_id(uid) == 0
-        obj = [bytes(uid)]
-        dist.broadcast_object_list(obj, src=0)
-        uid = (C.c_char * 128).from_buffer_copy(obj[0])
-        comm = C.c_void_p()
-        rc = L.pft_comm_init_rccl(C.byref(comm), world, rank, uid, dev)
-        if rc:
-            sys.exit(f"rank {rank}: pft_comm_init_rccl failed ({rc})")
-        L.pft_comm_set_current(comm)
+        comm = make_comm(L, a.transport, world, rank, dev, dist)
     else:
         L.pft_hip_set_device(dev)
         if a.self_exchange:
-            uid = (C.c_char * 128)()
-            assert L.pft_comm_get_unique_id(uid) == 0
-            comm = C.c_void_p()
-            rc = L.pft_comm_init_rccl(C.byref(comm), 1, 0, uid, dev)
-            if rc:
-                sys.exit(f"pft_comm_init_rccl failed ({rc})")
+            comm = make_comm(L, a.transport, 1, 0, dev, None)
             assert L.pft_comm_set_self_exchange(comm, 1) == 0
-            L.pft_comm_set_current(comm)
     L.pft_solver_set_option(P.PFT_OPT_DEVICE, dev)
     L.pft_solver_set_option(P.PFT_OPT_ONE_STREAM, 0 if a.two_stream else (2 if a.comm_boundary else 1))
     L.pft_solver_set_option(P.PFT_OPT_WAVE, a.wave)
@@ -173,13 +166,19 @@ def main():
     cells_total = n1 * n2 * total_n3
     final_time = base["final_time"]
 
+    callbacks = []
+    if a.callback:
+        @P.SERVICE_FN
+        def service(final, s):
+            callbacks.append((s.contents.t, s.contents.h))   # RKService logs t and tau, then stat()s
+            return 0
+
+        sim.system.Service_Callback = C.cast(service, C.c_void_p).value
+
     # warm-up: uploads x once, builds the kernels' caches; W attempted steps
     rc = sim.solve_ex(final_time, max(1, a.warmup), P.PFT_SOLVE_KEEP_DEVICE)
     assert rc == 2, rc
     st0 = sim.system.steps_total
-    if not a.no_timing:
-        # every 10th attempted step: the event packets cost ~3 us per timed stage
-        L.pft_solver_set_option(P.PFT_OPT_TIMING, 10)
     barrier()
     t1 = time.perf_counter()
     timed_flags = 0 if a.host_boundary else P.PFT_SOLVE_KEEP_DEVICE | P.PFT_SOLVE_REUSE_DEVICE
@@ -195,6 +194,15 @@ def main():
         tt = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
+    accepted = int(sim.system.steps)
+    t_end = sim.t
+    # stage kernels timed in a separate pass after the timed region (HIP events on the slab's
+    # compute stream, every other attempted step: each timed stage adds an event pair)
+    if not a.no_timing and a.timing_steps > 0:
+        L.pft_solver_set_option(P.PFT_OPT_TIMING, 2)
+        rc = sim.solve_ex(final_time, a.timing_steps, P.PFT_SOLVE_KEEP_DEVICE | P.PFT_SOLVE_REUSE_DEVICE)
+        assert rc == 2, rc
+        L.pft_solver_set_option(P.PFT_OPT_TIMING, 0)
     stats = sim.stats()
     geo = sim.tile_geometry()
     L.pft_slab_get_gl_keep.argtypes = [C.c_void_p]
@@ -217,17 +225,21 @@ def main():
         dom = max(per, key=lambda s: per[s][0])
         ms, byts = per[dom]
         achieved = byts / (ms * 1e-3) / 1e9
-        traffic = None
+        traffic, traffic_src = None, None
         pmc = os.path.join(REPO, "profiles", "pmc_summary.json")
         if os.path.exists(pmc) and not a.wave:
             try:
                 ps = json.load(open(pmc))
                 key = f"stage{dom}_gl{int(a.gl_static)}_{n1}x{n2}x{sim.grid.n3}_m{a.mode}"
                 traffic = ps.get(key, {}).get("hbm_bytes_per_launch")
+                if traffic is not None:
+                    # not measured in this run: the calibrated FETCH_SIZE + WRITE_SIZE of that
+                    # kernel from the rocprofv3 --pmc passes recorded in the file
+                    traffic_src = dict(ps.get("provenance", {}), file="profiles/pmc_summary.json", key=key)
             except (OSError, ValueError):
                 traffic = None
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": kernel_name(dom, a, rc_path, n1),
                 "algorithmic_bytes_per_launch": byts // nl[dom],
                 "avg_launch_ms": round(ms / nl[dom], 4),
@@ -261,16 +273,18 @@ def main():
                    "grid_nodes": gn, "shape": a.shape, "literal_cube": a.literal_cube,
                    "calc_mode": a.mode, "cells": cells_total, "parallelism": f"zslab{world}",
                    "gl_static": a.gl_static, "kz": a.kz or "auto", "tile": a.tile, "recompute": not a.no_recompute,
-                   "accepted_steps_total": int(sim.system.steps), "t_end": sim.t,
+                   "accepted_steps_total": accepted, "t_end": t_end,
                    "host_boundary": a.host_boundary, "self_exchange": a.self_exchange,
+                   "transport": (a.transport if (world > 1 or a.self_exchange) else None),
+                   "service_callback": a.callback,
                    "pipeline": ("two-stream" if a.two_stream else "comm-boundary" if a.comm_boundary
                                 else "one-stream"), "wave": a.wave,
                    "gl_store_skipped": gl_keep,
                    "tiles": ({str(k): ("cache" if v[0] == 0 else f"{2 * v[1]}x{v[2]} cells")
                               for k, v in geo.items()} if geo else None)},
         "roofline": roof,
-        "fused_effective_GBps": round(step_bytes * cells_total * steps / el / 1e9 / world, 1),
-        "survey_840B_equiv_GBps": round(SURVEY_BYTES_PER_CELL_STEP * cells_total * steps / el / 1e9 / world, 1),
+        # whole step at its algorithmic bytes (39 doubles per cell-step), per GPU
+        "step_algorithmic_GBps": round(step_bytes * cells_total * steps / el / 1e9 / world, 1),
         "init_s": round(init_s, 2),
     }
 
@@ -302,6 +316,30 @@ def main():
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist is not None:
         dist.destroy_process_group()
+
+
+def make_comm(L, transport, world, rank, dev, dist):
+    """libpft communicator of this rank (pft_comm.h), bound to this thread.  The rendezvous data
+    (ipc: a shared-memory name, rccl: the unique id) goes through torch.distributed's gloo store."""
+    comm = C.c_void_p()
+    if transport == "ipc":
+        name = [f"/pft_bench_{os.getpid()}_{int(time.time() * 1e6) % 10**9}"]
+        if dist is not None:
+            dist.broadcast_object_list(name, src=0)
+        rc = L.pft_comm_init_ipc(C.byref(comm), world, rank, name[0].encode(), dev)
+    else:
+        uid = (C.c_char * 128)()
+        if rank == 0:
+            assert L.pft_comm_get_unique_id(uid) == 0
+        if dist is not None:
+            obj = [bytes(uid)]
+            dist.broadcast_object_list(obj, src=0)
+            uid = (C.c_char * 128).from_buffer_copy(obj[0])
+        rc = L.pft_comm_init_rccl(C.byref(comm), world, rank, uid, dev)
+    if rc:
+        sys.exit(f"rank {rank}: pft_comm_init_{transport} failed ({rc})")
+    L.pft_comm_set_current(comm)
+    return comm
 
 
 def workload(grid_nodes, world, shape="cube", literal_cube=False, mode=0, domain=None):
@@ -373,10 +411,21 @@ def cpu_baseline(sim, base, a):
     el = run(n)
     cores = int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count() or 1)))
     cells = g.n1 * g.n2 * g.total_n3
-    return {"value": round(cells * stt.value / el / 1e6, 3), "unit": "Mcells·steps/s", "cores": cores,
-            "kind": "port",
-            "sample": f"{stt.value} attempted steps of the same {g.n1}x{g.n2}x{g.total_n3} state (after 3 untimed), "
-                      f"oracle/pft_oracle.c (gcc -O2, OpenMP {cores} threads), {el:.1f} s"}
+    value = cells * stt.value / el / 1e6
+    out = {"value": round(value, 3), "unit": "Mcells·steps/s", "cores": cores, "kind": "port",
+           "sample": f"{stt.value} attempted steps of the same {g.n1}x{g.n2}x{g.total_n3} state (after 3 untimed), "
+                     f"oracle/pft_oracle.c (gcc -O2, OpenMP {cores} threads), {el:.1f} s"}
+    # the port's speed relative to the reference itself, measured on the same cores and state in the
+    # build container (scripts/calibrate_cpu.py: the reference compiled in place, P MPI ranks x 1
+    # thread, vs the port on P threads, same attempted steps, bitwise-equal result)
+    cal = os.path.join(REPO, "profiles", "r02_cpu_calibration.json")
+    if os.path.exists(cal):
+        c = json.load(open(cal))
+        out["reference_equivalent"] = {
+            "value": round(value * c["reference_over_port"], 3), "factor": c["reference_over_port"],
+            "calibration": f"profiles/r02_cpu_calibration.json: reference {c['reference']['Mcells_steps_per_s']} vs "
+                           f"port {c['port']['Mcells_steps_per_s']} Mcells*steps/s on {c['cores']} cores, {c['grid']}"}
+    return out
 
 
 if __name__ == "__main__":

@@ -29,7 +29,7 @@
  *        as solve, with RK_MPI_SA_handle_NAN(handle_nan) (hybrid2.c:138-166) and, when break_at
  *        >= 0, a Service_Callback (hybrid2.c:670-705) that logs every call (steps, t, h) to
  *        <outdir>/cb.txt and returns 1 on its break_at-th call (0 = never); traj.txt rows gain
- *        RK_MPI_SA_check_NAN()
+ *        RK_MPI_SA_check_NAN(); <outdir>/wall<i>.txt holds the wall seconds of call i
  */
 
 #include "common.h"
@@ -350,7 +350,13 @@ int main(int argc, char ** argv)
 				}
 			}
 			for(call=first_T; call<argc; call++) {
+				double w0 = MPI_Wtime(), w1;
 				int rc = RK_MPI_SA_solve(strtod(argv[call], NULL), &sys);
+				w1 = MPI_Wtime();
+				if(ext && MPIrank==0) {   /* wall time of the call (the CPU-baseline calibration) */
+					FILE * wf; sprintf(path, "%s/wall%d.txt", argv[3], call-first_T);
+					if((wf = fopen(path, "w"))) { fprintf(wf, "%.6f\n", w1 - w0); fclose(wf); }
+				}
 				if(tf && ext) fprintf(tf, "%a %a %ld %ld %d %d\n", sys.t, sys.h, sys.steps, sys.steps_total, rc, RK_MPI_SA_check_NAN());
 				else if(tf) fprintf(tf, "%a %a %ld %ld %d\n", sys.t, sys.h, sys.steps, sys.steps_total, rc);
 				sprintf(path, "%s/state%d.f64", argv[3], call-first_T); gather_write(solution, path);

@@ -33,7 +33,7 @@ enum { KIND_SELF = 0, KIND_RCCL = 1, KIND_LOOP = 2, KIND_IPC = 3 };
 #define PFT_IPC_MAGIC 0x7066745f69706331ULL   // "pft_ipc1"
 
 struct IpcSlot {              // one rank's slab, published at attach
-  int n3;
+  int n3, device;
   long fs;
   char handles[PFT_IPC_HANDLE_BYTES];
 };
@@ -365,19 +365,20 @@ static int ipc_attach(pft_comm* c, pft_slab* s)
   IpcSlot* me = &c->shm->slot[c->rank];
   if ((rc = pft_slab_ipc_export(s, me->handles))) return rc;
   me->n3 = pft_slab_nz(s);
+  me->device = c->device;
   me->fs = (long)pft_slab_field_stride(s);
   if ((rc = ipc_round(c, nullptr, 0, nullptr, 0, &recs))) return rc;   // every slot is published
   if (c->self_x) {
-    if ((rc = pft_slab_ipc_set_peer(s, 0, nullptr, 0, 0)) || (rc = pft_slab_ipc_set_peer(s, 1, nullptr, 0, 0)))
+    if ((rc = pft_slab_ipc_set_peer(s, 0, nullptr, 0, 0, 0)) || (rc = pft_slab_ipc_set_peer(s, 1, nullptr, 0, 0, 0)))
       return rc;
   } else {
     if (c->rank > 0) {
       const IpcSlot* b = &c->shm->slot[c->rank - 1];
-      if ((rc = pft_slab_ipc_set_peer(s, 0, b->handles, b->n3, b->fs))) return rc;
+      if ((rc = pft_slab_ipc_set_peer(s, 0, b->handles, b->n3, b->fs, b->device))) return rc;
     }
     if (c->rank < c->size - 1) {
       const IpcSlot* a = &c->shm->slot[c->rank + 1];
-      if ((rc = pft_slab_ipc_set_peer(s, 1, a->handles, a->n3, a->fs))) return rc;
+      if ((rc = pft_slab_ipc_set_peer(s, 1, a->handles, a->n3, a->fs, a->device))) return rc;
     }
   }
   // the slots are reused by the next attach only after everyone has read them
@@ -416,7 +417,7 @@ static int halo_start(pft_comm* c, int buf, int f0, int f1, bool on_comm)
     // stream-ordered on the compute stream: put (boundary planes into the neighbours' ghost
     // planes, then their flags), then wait for our own flags
     const unsigned long long seq = ++c->dseq;
-    int rc = pft_slab_halo_put(s, buf, f0, f1, seq);
+    int rc = pft_slab_take_pushed(s, buf) ? pft_slab_halo_signal(s, seq) : pft_slab_halo_put(s, buf, f0, f1, seq);
     return rc ? rc : pft_slab_halo_wait(s, seq);
   }
   if (c->kind == KIND_RCCL) {

@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/pft_hip.h"
@@ -292,7 +293,14 @@ struct StageArgs {
   double cin;          // coefficient of the stage-input combine: h3, h6, h8, h for stages 2..5
   int gwx, gty;        // merson_fused tile: gwx cell pairs x gty rows (fused_geometry)
   int gl_keep;         // stage 5: x(t+h) of gl is not stored, XN already holds it (pft_slab_set_gl_keep)
+  // ipc transport (merson_fused): the output's boundary planes are also stored into the
+  // neighbours' ghost planes -- plane 0 to plo (the neighbour below's top ghost plane, field 0),
+  // plane n3-1 to phi (the neighbour above's bottom ghost plane); null: no neighbour that side
+  double* plo;
+  double* phi;
+  long plo_fs, phi_fs;
 };
+
 
 __device__ __forceinline__ int xcd_remap(int b, int n)
 {
@@ -535,6 +543,13 @@ __device__ __forceinline__ void st2(double* p, dbl2 v)
   *reinterpret_cast<dbl2*>(p) = v;
 #endif
 }
+// a boundary plane's output pair also goes to the z-neighbour's ghost plane (ipc transport)
+__device__ __forceinline__ void push2(const StageArgs& a, int k, int q, long po, dbl2 v)
+{
+  if (k == 0 && a.plo) st2(a.plo + q * a.plo_fs + po, v);
+  if (k == a.n3 - 1 && a.phi) st2(a.phi + q * a.phi_fs + po, v);
+}
+
 // store a pair with its halves exchanged when sw = 1 (two 8-byte stores at per-thread offsets)
 __device__ __forceinline__ void st2x(double* p, dbl2 v, int sw)
 {
@@ -772,7 +787,9 @@ __device__ __forceinline__ void keep5(int q, const Ops& r, dbl2& x, dbl2& k1, db
   for (int s = 0; s < 2; ++s) E[s] = 0.2 * r.k1[s] - 0.9 * r.k3[s] + 0.8 * r.k4[s];   // hybrid2.c:521 prefix
 }
 
-template <int STAGE, int MODE, bool GLS>
+// PUSH (ipc transport): the output's boundary planes also go to the z-neighbours' ghost planes;
+// a separate instantiation, so that the single-slab kernels carry no extra registers
+template <int STAGE, int MODE, bool GLS, bool PUSH = false>
 __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT_S5_WAVES2 && STAGE == 5) || ((GLS || PFT_DEEP_ALL) && ((PFT_DEEP_MASK >> STAGE) & 1)) ? 2 : PFT_FUSED_WAVES))) void merson_fused(StageArgs a, pft_consts c)
 {
   // tile geometry chosen by the host per grid (fused_geometry): gwx pairs x gty rows, so that the
@@ -1026,6 +1043,20 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT
     }
   }
 
+  if constexpr (PUSH) {
+    // the output's boundary planes, stored by this very thread in the march above, also go to the
+    // z-neighbours' ghost planes: read back (own stores, L2-hot) and stored once the march is
+    // over, so the march itself holds no extra registers.  The fields are the ones stored.
+    if (active && kb < ke) {
+      const double* dst = STAGE == 5 ? a.out : a.kout;
+      const int nq = (GLS || (STAGE <= 4 && PFT_GLK_LITERAL) || (STAGE == 5 && a.gl_keep)) ? 2 : 3;
+      for (int q = 0; q < nq; ++q) {
+        if (kb == 0 && a.plo) push2(a, 0, q, po, ld2(dst + q * a.fs + a.plane + po));
+        if (ke == a.n3 && a.phi) push2(a, a.n3 - 1, q, po, ld2(dst + q * a.fs + (long)a.n3 * a.plane + po));
+      }
+    }
+  }
+
   if (STAGE == 5) {
     __shared__ double red[PFT_FBLOCK / 64];
     __shared__ int rnf[PFT_FBLOCK / 64];
@@ -1172,10 +1203,6 @@ struct PutArgs {
   long dlo_fs;
   double* dhi;                // the neighbour above: its bottom ghost plane (0) of field 0, or null
   long dhi_fs;
-  unsigned long long* slo;    // the neighbour below's flag "from above"
-  unsigned long long* shi;    // the neighbour above's flag "from below"
-  unsigned int* count;        // workgroups done (this slab's own memory)
-  unsigned long long seq;
 };
 
 __global__ __launch_bounds__(256) void halo_put_kernel(PutArgs a)
@@ -1192,16 +1219,19 @@ __global__ __launch_bounds__(256) void halo_put_kernel(PutArgs a)
       if (a.dhi) a.dhi[(a.f0 + f) * a.dhi_fs + c] = a.src[(a.f0 + f) * a.fs + (long)a.n3 * a.plane + c];  // plane n3
     }
   }
-  // every workgroup's stores are visible system-wide before it is counted; the last one counted
-  // raises the flags (release), so a neighbour that sees the flag sees the whole plane
-  __threadfence_system();
-  __syncthreads();
-  if (threadIdx.x == 0 && atomicAdd(a.count, 1u) == gridDim.x - 1) {
-    atomicExch(a.count, 0u);
-    __threadfence_system();
-    if (a.slo) __hip_atomic_store(a.slo, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (a.shi) __hip_atomic_store(a.shi, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+}
+
+// raises the neighbours' flags once the kernels before it on the stream (the put, or a stage
+// kernel that stored its boundary planes into the neighbours' ghost planes) have completed: their
+// stores are released at kernel end; with a neighbour on another GPU a system-scope fence first
+// (the flag must not overtake the plane over xGMI).  One thread, vector atomics only.
+__global__ void halo_signal_kernel(unsigned long long* slo, unsigned long long* shi, unsigned long long seq,
+                                   int remote)
+{
+  if (threadIdx.x != 0) return;
+  if (remote) __threadfence_system();
+  if (slo) __hip_atomic_store(slo, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (shi) __hip_atomic_store(shi, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1226,6 +1256,7 @@ struct SlabPeer {
   unsigned long long* sig;             // the neighbour's flag words
   long fs;                             // its field stride
   int n3;                              // its interior planes
+  int remote;                          // 1: on another GPU (xGMI)
 };
 
 struct pft_slab {
@@ -1240,6 +1271,9 @@ struct pft_slab {
   unsigned long long* sig;       // flag words written by the neighbours: [0] from below, [1] from
                                  // above (monotonic exchange sequence numbers); [8] put counter
   SlabPeer peer[2];              // [0] the neighbour below, [1] above
+  int fused_push;                // ipc: the fused kernels push (PFT_IPC_FUSED_PUSH, default 0)
+  int pushed_role;               // buffer role whose boundary planes the last stage launch pushed
+                                 // into the neighbours (merson_fused), -1: none
   double* staging;       // host padded layout on the device (for upload/download)
   long S;                // host padded block (one field)
   unsigned long long* scratch;  // [0] eps bits, [1] nonfinite flag
@@ -1310,6 +1344,16 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
   s->tile_wx = 1;
   s->n1_tiled_ok = 1;
   s->recompute = 1;
+  s->pushed_role = -1;
+  {
+    // ipc transport: 0 (default) = a separate put kernel after each stage; 1 = the fused stage
+    // kernels store their boundary planes into the neighbours after their z-march (PUSH
+    // instantiation).  Measured on the 400x400x100 / 318x318x159 / 252^3 / 200x200x400 rank slabs
+    // (scripts/ab_transport.sh, self exchange, two rounds): the put kernel cost 3-6% per rank, the
+    // push inside the stage kernels 5-9% (its boundary workgroups finish last)
+    const char* e = getenv("PFT_IPC_FUSED_PUSH");
+    s->fused_push = e ? atoi(e) : 0;
+  }
   const size_t bytes = sizeof(double) * 3 * (size_t)s->fs;
   hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
 #if PFT_COMM_HIPRIO
@@ -1410,6 +1454,7 @@ static int ensure_staging(pft_slab* s)
 
 int pft_slab_upload_host(pft_slab* s, int which, const double* host_padded)
 {
+  s->pushed_role = -1;
   // X and XN may differ now: the caller re-establishes it (an upload of a stage buffer, e.g. A0
   // for a host-side RHS evaluation, leaves it alone)
   if (which == PFT_BUF_X || which == PFT_BUF_XN) s->gl_keep = 0;
@@ -1489,6 +1534,12 @@ template <int STAGE, int MODE, bool GLS>
 static void launch_kernel(int kind, int wx, dim3 g, hipStream_t st, const StageArgs& a, const pft_consts& c)
 {
   if (kind == KFUSED) {
+    if constexpr (STAGE >= 1) {
+      if (a.plo || a.phi) {
+        merson_fused<STAGE, MODE, GLS, true><<<g, PFT_FBLOCK, 0, st>>>(a, c);
+        return;
+      }
+    }
     merson_fused<STAGE, MODE, GLS><<<g, PFT_FBLOCK, 0, st>>>(a, c);
   } else if (kind == KTILE) {
     if (wx == 16)
@@ -1718,6 +1769,27 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   // stage-input coefficients of the recompute path: exactly the solver's h/3.0, h/6.0, h/8.0, h
   a.cin = stage == 2 ? h / 3.0 : stage == 3 ? h / 6.0 : stage == 4 ? h / 8.0 : h;
   if (kind == KFUSED && in) a.x = in;    // pure RHS / speculative stage 1: the input is the given buffer
+  // ipc transport: the fused kernel stores the output's boundary planes into the neighbours' ghost
+  // planes too (the buffer of the same role there: every rank swaps identically)
+  s->pushed_role = -1;
+  double* dst = stage == 5 ? out : kout;
+  if (kind == KFUSED && stage >= 1 && dst && s->fused_push && (s->peer[0].on || s->peer[1].on) && !bnd) {
+    int role = -1;
+    for (int r = 0; r < PFT_BUF_COUNT; ++r)
+      if (s->buf[r] == dst) role = r;
+    if (role >= 0) {
+      const int ph = s->phys[role];
+      if (s->peer[0].on) {
+        a.plo = s->peer[0].base[ph] + (long)(s->peer[0].n3 + 1) * s->plane;
+        a.plo_fs = s->peer[0].fs;
+      }
+      if (s->peer[1].on) {
+        a.phi = s->peer[1].base[ph];
+        a.phi_fs = s->peer[1].fs;
+      }
+      s->pushed_role = role;
+    }
+  }
   // gl's x(t+h) is x + coef*(0.5*(0.0 + 0.0) + 2.0*0.0) (gl's K's are literal zeros): equal to x
   // bit for bit when coef is finite and no gl value is -0.0 or NaN, which the solver checked at
   // upload (pft_slab_set_gl_keep); XN's gl then already holds it, and stage 5 skips that store
@@ -1963,7 +2035,7 @@ int pft_slab_ipc_export(pft_slab* s, void* handles)
   return 0;
 }
 
-int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, long fs)
+int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, long fs, int device)
 {
   if (side < 0 || side > 1) return -2;
   SlabPeer& p = s->peer[side];
@@ -1992,6 +2064,9 @@ int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, lo
   }
   p.n3 = n3;
   p.fs = fs;
+  int mine = 0;
+  HIPCHK(hipGetDevice(&mine));
+  p.remote = device != mine;
   p.opened = 1;
   p.on = 1;
   return 0;
@@ -2025,21 +2100,34 @@ int pft_slab_halo_put(pft_slab* s, int role, int f0, int f1, unsigned long long 
   if (s->peer[0].on) {
     a.dlo = s->peer[0].base[ph] + (long)(s->peer[0].n3 + 1) * s->plane;
     a.dlo_fs = s->peer[0].fs;
-    a.slo = s->peer[0].sig + 1;
   }
   if (s->peer[1].on) {
     a.dhi = s->peer[1].base[ph];
     a.dhi_fs = s->peer[1].fs;
-    a.shi = s->peer[1].sig + 0;
   }
-  if (!a.slo && !a.shi) return 0;
-  a.count = (unsigned int*)(s->sig + 8);
-  a.seq = seq;
+  if (!a.dlo && !a.dhi) return 0;
   const long n = 2L * a.nf * s->plane;
   const int blocks = (int)std::min<long>(1024, std::max<long>(1, (n + 255) / 256));
   halo_put_kernel<<<blocks, 256, 0, s->stream>>>(a);
   HIPCHK(hipGetLastError());
+  return pft_slab_halo_signal(s, seq);
+}
+
+int pft_slab_halo_signal(pft_slab* s, unsigned long long seq)
+{
+  unsigned long long* slo = s->peer[0].on ? s->peer[0].sig + 1 : nullptr;   // below: its "from above"
+  unsigned long long* shi = s->peer[1].on ? s->peer[1].sig + 0 : nullptr;   // above: its "from below"
+  if (!slo && !shi) return 0;
+  halo_signal_kernel<<<1, 64, 0, s->stream>>>(slo, shi, seq, s->peer[0].remote || s->peer[1].remote);
+  HIPCHK(hipGetLastError());
   return 0;
+}
+
+int pft_slab_take_pushed(pft_slab* s, int role)
+{
+  const int r = s->pushed_role;
+  s->pushed_role = -1;
+  return r >= 0 && r == role;
 }
 
 int pft_slab_halo_wait(pft_slab* s, unsigned long long seq)

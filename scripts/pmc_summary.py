@@ -66,6 +66,12 @@ def main(trace_dir, fetch_dir, write_dir, dims, probe_bytes, out_path):
         res[key] = {"kernel": k, "fetch_bytes": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
                     "raw_FETCH_SIZE_KiB": fetch.get(k), "raw_WRITE_SIZE_KiB": write.get(k)}
     res["kernel_stats"] = stats
+    # where these numbers come from (bench.py copies this into roofline.traffic_source)
+    res["provenance"] = {"tool": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes of "
+                                 "bench.py (scripts/evidence.sh); FETCH_SIZE x fetch_factor from the probe copy",
+                         "tag": os.environ.get("TAG", ""),
+                         "date": os.environ.get("PMC_DATE", ""),
+                         "git": os.environ.get("PMC_GIT", "")}
     with open(out_path, "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
     print(json.dumps({k: v.get("hbm_bytes_per_launch") for k, v in res.items() if isinstance(v, dict)}, indent=1))
