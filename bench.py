@@ -81,10 +81,12 @@ def parse():
     ap.add_argument("--host-boundary", action="store_true",
                     help="timed call is one RK_MPI_SA_solve-style call: x copied host->device at entry "
                          "and back at exit (PCIe-inclusive rate; never the headline value)")
-    ap.add_argument("--transport", choices=("ipc", "rccl"), default="ipc",
+    ap.add_argument("--transport", choices=("auto", "ipc", "rccl"), default="auto",
                     help="N>1 (and --self-exchange) inter-slab transport (pft_comm.h): ipc = IPC-mapped "
-                         "neighbour slabs, boundary planes stored into their ghost planes + flag words "
-                         "(default); rccl = ncclSend/ncclRecv on a priority stream beside the interior sweep")
+                         "neighbour slabs, boundary planes stored into their ghost planes + flag words; "
+                         "rccl = ncclSend/ncclRecv on a priority stream beside the interior sweep; auto "
+                         "(default) = rccl with one GPU per rank, ipc when ranks share a GPU (RCCL refuses "
+                         "that) and for --self-exchange (DESIGN section 6)")
     ap.add_argument("--self-exchange", action="store_true",
                     help="diagnostic, 1 GPU: run the N>1 path of --transport (ipc: put kernel + flag waits "
                          "per stage; rccl: boundary planes first, halo exchange beside the interior sweep, "
@@ -130,6 +132,8 @@ def main():
     if ndev < 1:
         sys.exit("no HIP device visible (the benchmark has no CPU fallback)")
     dev = local % ndev           # one process per GPU; more ranks than GPUs share round-robin
+    if a.transport == "auto":
+        a.transport = "ipc" if (world > ndev or a.self_exchange) else "rccl"
     dist = None
     comm = None
     if world > 1:

@@ -162,6 +162,11 @@ int pft_slab_eps_mark(pft_slab * s);
 /* the same publication enqueued on another stream of the slab's device (the communication
    stream, behind the eps max over ranks: pft_comm_eps_publish) */
 int pft_slab_eps_mark_on(pft_slab * s, void * stream);
+/* 1: a stage-5 launch over the whole slab publishes the error norm itself (its last workgroup
+   writes it to pinned host memory, which pft_slab_eps_fetch polls) and pft_slab_eps_mark adds no
+   kernel; for the single-rank and ipc paths, where the max over ranks is not a device
+   collective */
+int pft_slab_set_inkernel_publish(pft_slab * s, int on);
 
 /* generic chunk-table combines for the host-staged path (any RK_MEM_DIST on a flat array) */
 int pft_flat_alloc(double ** p, size_t n);
@@ -187,13 +192,19 @@ int pft_probe_copy(double * dst, const double * src, size_t n, void * stream);
    set_peer(side 0 = below / 1 = above): open the neighbour's handles (handles = NULL: the slab
    itself, the one-GPU self-exchange diagnostic); n3 / fs are the neighbour's planes and stride;
    halo_put: boundary planes 1 and n3 of buffer `role`, fields [f0, f1), into the neighbours' ghost
-   planes, then `seq` into their flag words (one kernel on the compute stream);
+   planes, then `seq` into their flag words (a copy and a one-thread signal kernel on the compute
+   stream);
    halo_wait: the compute stream waits until both neighbours' flags reach `seq`. */
 #define PFT_IPC_HANDLE_BYTES (64 * (PFT_BUF_COUNT + 1))
 int pft_slab_ipc_export(pft_slab * s, void * handles);
-int pft_slab_ipc_set_peer(pft_slab * s, int side, const void * handles, int n3, long fs);
+int pft_slab_ipc_set_peer(pft_slab * s, int side, const void * handles, int n3, long fs, int device);
 int pft_slab_ipc_close(pft_slab * s);
 int pft_slab_halo_put(pft_slab * s, int role, int f0, int f1, unsigned long long seq);
+/* raise the neighbours' flags to `seq` behind the work on the compute stream (halo_put calls it) */
+int pft_slab_halo_signal(pft_slab * s, unsigned long long seq);
+/* 1 when the last stage launch already stored the boundary planes of buffer `role` into the
+   neighbours' ghost planes (the fused kernel does, with neighbours set); clears the mark */
+int pft_slab_take_pushed(pft_slab * s, int role);
 int pft_slab_halo_wait(pft_slab * s, unsigned long long seq);
 
 /* peer copy of one ghost plane between slabs on the same process (loopback transport) */

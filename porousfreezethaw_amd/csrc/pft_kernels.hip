@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -36,6 +37,7 @@
 #define PFT_FBLOCK 256
 #endif
 #define PFT_TRING 8
+#define PFT_PUB_SLOTS 64
 
 // recompute path: the gl components of K1..K4 are the literal zeros of dgl (equation.c:731,874),
 // not arrays in HBM (42 instead of 54 doubles per cell-step, bit-identical).  An A/B build with
@@ -299,7 +301,15 @@ struct StageArgs {
   double* plo;
   double* phi;
   long plo_fs, phi_fs;
+  // stage 5 (merson_fused): the last workgroup to finish publishes the error norm straight to
+  // pinned host memory (pub[0] eps bits, pub[1] non-finite flag, both pre-set to a sentinel by
+  // the host) and resets the accumulator; pub_count counts the finished workgroups
+  unsigned long long* pub;
+  unsigned int* pub_count;
 };
+
+// a value the error norm never takes (a NaN pattern: the max skips NaN) nor the flag
+#define PFT_PUB_SENTINEL 0xFFF8DEADBEEF0001ULL
 
 
 __device__ __forceinline__ int xcd_remap(int b, int n)
@@ -1081,6 +1091,19 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT
       }
       if (bm > 0.0) atomicMax(a.eps_bits, (unsigned long long)__double_as_longlong(bm));
       if (bnf) atomicOr(a.nonfinite, 1u);
+      if (a.pub) {
+        // this workgroup's atomics are performed (memory-side) before it is counted; the last one
+        // counted reads the final max, resets the accumulator and publishes both words to the
+        // host, which polls them (no publish kernel, no event: pft_slab_eps_fetch)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (atomicAdd(a.pub_count, 1u) == gridDim.x - 1) {
+          const unsigned long long e = atomicExch(a.eps_bits, 0ULL);
+          const unsigned int f = atomicExch(a.nonfinite, 0u);
+          atomicExch(a.pub_count, 0u);
+          __hip_atomic_store(a.pub, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(a.pub + 1, (unsigned long long)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
     }
   }
 }
@@ -1286,7 +1309,17 @@ struct pft_slab {
   hipEvent_t ev_order[3];  // stream-order events: [0] compute -> comm, [1] comm -> compute,
                            // [2] the last boundary launch on the comm stream
   hipEvent_t ev_eps;     // recorded on the compute stream after the error norm is final
-  int eps_marked;
+  int eps_marked;        // 1: publish kernel + event; 2: published by stage 5 itself (pub ring)
+  // in-kernel publication (pft_slab_set_inkernel_publish): ring of 2-word slots in pinned,
+  // coherent host memory, one per stage-5 launch; the host pre-sets a slot to the sentinel and
+  // polls it after the launch
+  int inkernel_pub;
+  unsigned long long* pub_ring;      // host address (PFT_PUB_SLOTS x 2 words)
+  unsigned long long* pub_ring_dev;  // its device address
+  unsigned int* pub_count;           // device: finished workgroups of the publishing launch
+  long pub_next;                     // slots used so far
+  int pub_armed;                     // the last stage-5 launch publishes into slot pub_slot
+  int pub_slot;
   int kz;                // planes per workgroup z-march; 0 = automatic (z-chunk cost model)
   int n_cu;               // compute units of the slab's device
   double* noise;         // device u_noise (n3*plane) or null
@@ -1374,7 +1407,15 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
   if (e == hipSuccess) e = hipHostMalloc((void**)&s->host_scratch, 64, hipHostMallocDefault);
   if (e == hipSuccess) e = hipHostMalloc((void**)&s->host_pub, 64, hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&s->host_pub_dev, s->host_pub, 0);
-  if (e == hipSuccess) e = hipMalloc((void**)&s->sig, 4096);
+  if (e == hipSuccess)
+    e = hipHostMalloc((void**)&s->pub_ring, 16 * PFT_PUB_SLOTS, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&s->pub_ring_dev, s->pub_ring, 0);
+  if (e == hipSuccess) e = hipMalloc((void**)&s->pub_count, 64);
+  if (e == hipSuccess) e = hipMemsetAsync(s->pub_count, 0, 64, s->stream);
+  // the flag words are polled by the command processor (hipStreamWaitValue64) and written by a
+  // neighbour -- possibly another GPU over xGMI: uncached device memory, so that no cache between
+  // the writer and the poller can hold a stale copy
+  if (e == hipSuccess) e = hipExtMallocWithFlags((void**)&s->sig, 4096, hipDeviceMallocUncached);
   if (e == hipSuccess) e = hipMemsetAsync(s->sig, 0, 4096, s->stream);
   for (int b = 0; b < PFT_BUF_COUNT && e == hipSuccess; ++b) {
     e = hipMalloc((void**)&s->buf[b], bytes);
@@ -1412,6 +1453,8 @@ int pft_slab_destroy(pft_slab* s)
   if (s->scratch) (void)hipFree(s->scratch);
   if (s->host_scratch) (void)hipHostFree(s->host_scratch);
   if (s->host_pub) (void)hipHostFree(s->host_pub);
+  if (s->pub_ring) (void)hipHostFree(s->pub_ring);
+  if (s->pub_count) (void)hipFree(s->pub_count);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   if (s->comm) (void)hipStreamDestroy(s->comm);
   if (s->side) (void)hipStreamDestroy(s->side);
@@ -1797,6 +1840,18 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   a.em0 = s->d.eps_mult[0];
   a.em1 = s->d.eps_mult[1];
   a.em2 = s->d.eps_mult[2];
+  s->pub_armed = 0;
+  if (stage == 5 && kind == KFUSED && out && !bnd && k_begin == 0 && k_end == s->d.n3 && s->inkernel_pub) {
+    // the whole slab in one launch: its last workgroup publishes the error norm (slot pre-set to
+    // the sentinel here, before the launch; the host polls it in pft_slab_eps_fetch)
+    const int j = (int)(s->pub_next % PFT_PUB_SLOTS);
+    __atomic_store_n(&s->pub_ring[2 * j], PFT_PUB_SENTINEL, __ATOMIC_RELEASE);
+    __atomic_store_n(&s->pub_ring[2 * j + 1], PFT_PUB_SENTINEL, __ATOMIC_RELEASE);
+    a.pub = s->pub_ring_dev + 2 * j;
+    a.pub_count = s->pub_count;
+    s->pub_armed = 1;
+    s->pub_slot = j;
+  }
   dim3 g((unsigned)(a.ntile * a.nchunk));
   const hipStream_t st = s->launch_comm ? s->comm : s->stream;
   if (gls)
@@ -1905,8 +1960,22 @@ int pft_slab_eps_reset(pft_slab* s)
 
 int pft_slab_eps_mark(pft_slab* s) { return pft_slab_eps_mark_on(s, (void*)s->stream); }
 
+int pft_slab_set_inkernel_publish(pft_slab* s, int on)
+{
+  s->inkernel_pub = on ? 1 : 0;
+  s->pub_armed = 0;
+  return 0;
+}
+
 int pft_slab_eps_mark_on(pft_slab* s, void* stream)
 {
+  if (s->pub_armed && stream == (void*)s->stream) {
+    // the stage-5 launch just enqueued publishes the error norm itself
+    s->pub_armed = 0;
+    s->pub_next++;
+    s->eps_marked = 2;
+    return 0;
+  }
   // the error norm goes to coherent pinned host memory by a one-thread kernel (which also resets
   // it for the next step), and an event marks its completion: the host waits for that event
   // only, never for a copy queued behind (or beside) the speculative stage-1 kernel that follows
@@ -1920,7 +1989,28 @@ int pft_slab_eps_mark_on(pft_slab* s, void* stream)
 
 int pft_slab_eps_fetch(pft_slab* s, double* eps, int* nonfinite)
 {
-  if (s->eps_marked) {
+  if (s->eps_marked == 2) {
+    // published by the stage-5 kernel: poll the slot (pinned, coherent) until both words left the
+    // sentinel; the speculative stage 1 behind it keeps running
+    s->eps_marked = 0;
+    volatile unsigned long long* w = s->pub_ring + 2 * s->pub_slot;
+    long spins = 0;
+    while (__atomic_load_n(&w[0], __ATOMIC_ACQUIRE) == PFT_PUB_SENTINEL ||
+           __atomic_load_n(&w[1], __ATOMIC_ACQUIRE) == PFT_PUB_SENTINEL) {
+      if (++spins < 200000) {
+        __builtin_ia32_pause();
+      } else if ((spins & 1023) == 0) {
+        // long wait: make sure the stream is alive (a fault ends here with its error)
+        const hipError_t q = hipStreamQuery(s->stream);
+        if (q != hipSuccess && q != hipErrorNotReady) return fail(q, "hipStreamQuery (error norm poll)");
+        if (q == hipSuccess && __atomic_load_n(&w[1], __ATOMIC_ACQUIRE) == PFT_PUB_SENTINEL)
+          return fail(hipErrorUnknown, "error norm never published");
+        sched_yield();
+      }
+    }
+    s->host_scratch[0] = w[0];
+    s->host_scratch[1] = w[1];
+  } else if (s->eps_marked) {
     // read back on the side stream: work enqueued on the compute stream after the mark (the
     // speculative stage 1 of the next step) keeps running while the host decides
     s->eps_marked = 0;

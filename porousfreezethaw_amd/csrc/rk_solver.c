@@ -404,6 +404,15 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	   are unchanged, so the current K1 is still exactly f(t, x) -- the reference recomputes the
 	   same bits (hybrid2.c:373) -- and the speculative one is dropped. */
 	spec = pft_slab_can_speculate(R.slab);
+	/* the error norm goes to the host from stage 5 itself (no publish kernel, no event) where no
+	   device collective sits between stage 5 and the host (one slab, or ipc); env
+	   PFT_INKERNEL_PUBLISH=0 turns it off (A/B) */
+	{
+		const char * e = getenv("PFT_INKERNEL_PUBLISH");
+		const int on = spec && R.opt_wave == 0 && (!pft_comm_splits(c) || pft_comm_device_halo(c)) &&
+		               !(e && atoi(e) == 0);
+		pft_slab_set_inkernel_publish(R.slab, on);
+	}
 
 	while(1) {
 		h2 = h/2.0; h3 = h/3.0; h6 = h/6.0; h8 = h/8.0;                          /* :355 */
