@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU-box session producing the round's evidence (TAG=r01 by default):
+# One GPU-box session producing the round's evidence (TAG=r02 by default; PMC_GIT = the commit, passed in):
 #   1. pytest -m gpu, smoke()
 #   2. rocprofv3 --kernel-trace --stats of a short bench run, then FETCH_SIZE and WRITE_SIZE in
 #      separate --pmc passes (never combined with other tracing) -> profiles/pmc_summary.json
@@ -8,7 +8,8 @@
 # Every GPU step runs under its own time limit; a crash/fault/timeout ends the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-TAG=${TAG:-r01}
+TAG=${TAG:-r02}
+export TAG PMC_DATE=${PMC_DATE:-$(date -u +%F)} PMC_GIT=${PMC_GIT:-unknown}
 O=gpurun_out/ev
 mkdir -p $O/prof
 fatal() { local rc=$1; echo "[$2] exit $rc" | tee -a $O/status.log
@@ -29,12 +30,18 @@ timeout -k 10 300 python bench.py --steps 100 --no-cpu --mode 1 > $O/bench_mode1
 timeout -k 10 300 python bench.py --steps 100 --no-cpu --mode 2 > $O/bench_mode2.json 2>> $O/bench_var.err; fatal $? bench_mode2
 timeout -k 10 300 python bench.py --steps 100 --no-cpu --gl-static > $O/bench_gls.json 2>> $O/bench_var.err; fatal $? bench_gls
 timeout -k 10 600 python bench.py --steps 50 --no-cpu --literal-cube > $O/bench_cube64M.json 2>> $O/bench_var.err; fatal $? bench_cube
-# per-rank slabs of the N > 1 cube workloads on one GPU, plain and through the RCCL stage
-# pipeline with a self-exchanging 1-rank communicator (--self-exchange)
+# the small grids (BASELINE configs[0] and [2]) and the drop-in configuration with a Service_Callback
+timeout -k 10 300 python bench.py --steps 2000 --warmup 20 --no-cpu --grid-nodes 100 > $O/bench_g100.json 2>> $O/bench_var.err; fatal $? bench_g100
+timeout -k 10 300 python bench.py --steps 400 --no-cpu --grid-nodes 200 > $O/bench_g200.json 2>> $O/bench_var.err; fatal $? bench_g200
+timeout -k 10 300 python bench.py --steps 200 --no-cpu --callback > $O/bench_callback.json 2>> $O/bench_var.err; fatal $? bench_callback
+timeout -k 10 300 python bench.py --steps 200 --no-cpu --host-boundary > $O/bench_hostb.json 2>> $O/bench_var.err; fatal $? bench_hostb
+# per-rank slabs of the N > 1 cube workloads on one GPU, plain and through the N > 1 path of each
+# transport with a self-exchanging 1-rank communicator (--self-exchange)
 for dom in "400 0.06,0.06,0.015 n8" "318 0.06,0.06,0.03 n4" "252 0.06,0.06,0.06 n2"; do
   set -- $dom
   timeout -k 10 300 python bench.py --steps 100 --no-cpu --grid-nodes $1 --domain $2 > $O/bench_slab_$3.json 2>> $O/bench_var.err; fatal $? slab_$3
-  timeout -k 10 300 python bench.py --steps 100 --no-cpu --grid-nodes $1 --domain $2 --self-exchange > $O/bench_slab_$3_selfx.json 2>> $O/bench_var.err; fatal $? slab_$3_selfx
+  for tr in ipc rccl; do
+    timeout -k 10 300 python bench.py --steps 100 --no-cpu --grid-nodes $1 --domain $2 --self-exchange --transport $tr > $O/bench_slab_$3_selfx_$tr.json 2>> $O/bench_var.err; fatal $? slab_$3_selfx_$tr
+  done
 done
-timeout -k 10 300 python bench.py --steps 100 --no-cpu --self-exchange > $O/bench_selfx.json 2>> $O/bench_var.err; fatal $? bench_selfx
 echo done >> $O/status.log
