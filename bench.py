@@ -50,6 +50,10 @@ STAGE_DOUBLES_AUX = {False: {1: 9, 2: 12, 3: 15, 4: 18, 5: 18}, True: {1: 7, 2: 
 # stage 2 stores S = K1 + K2, so stage 3 reads x and S (PFT_K12_SUM); stage 5 stores gl's x(t+h)
 # only when it is not x itself (pft_slab_get_gl_keep: 11 doubles then, as with gl_static)
 STAGE_DOUBLES_RC = {False: {1: 5, 2: 7, 3: 7, 4: 9, 5: 12}, True: {1: 5, 2: 7, 3: 7, 4: 9, 5: 11}}
+# pair kernels (one slab, PFT_OPT_PAIR, merson_pair), timed as stages 3 and 5: pair 2+3 reads x and
+# K1 and writes K3 (K2 never stored), pair 4+5 reads x, K1, K3 and writes x(t+h) (K4 never stored);
+# with the speculative stage 1: 21 doubles per cell-step
+PAIR_DOUBLES = {False: {1: 5, 3: 7, 5: 10}, True: {1: 5, 3: 7, 5: 9}}
 METRIC = "Mcells·RK-steps/s at 400³ grid, 1/2/4/8 MI355X; % HBM roofline"
 PUBLISHED_400_MODE1 = 351.88      # BASELINE.md 1, CC-HR-12nodes SigmaP1-P-smallsigma, 384 cores
 
@@ -212,9 +216,12 @@ def main():
     L.pft_slab_get_gl_keep.argtypes = [C.c_void_p]
     L.pft_solver_slab.restype = C.c_void_p
     gl_keep = bool(rc_path and L.pft_slab_get_gl_keep(L.pft_solver_slab()))
+    pairs = bool(stats.pairs)
+    if pairs:
+        STAGE_DOUBLES = PAIR_DOUBLES
     if gl_keep and not a.gl_static:
         STAGE_DOUBLES = {g: dict(v) for g, v in STAGE_DOUBLES.items()}
-        STAGE_DOUBLES[False][5] = 11
+        STAGE_DOUBLES[False][5] = 9 if pairs else 11
 
     # ---- roofline: dominant fused stage kernel, HIP events on the slab's compute stream -----
     roof = None
@@ -223,6 +230,8 @@ def main():
         # wavefront (--wave): stages 2..5 are timed per launch, nl[s] launches of W planes per step
         nl = wave_launches(sim.grid.n3, a.wave) if a.wave and world == 1 else {s: 1 for s in range(1, 6)}
         for s in range(1, 6):
+            if stats.stage_n[s] == 0:
+                continue                                                 # a pair's first stage
             ms = stats.stage_ms[s] / max(1, stats.stage_n[s]) * nl[s]     # per step
             byts = STAGE_DOUBLES[a.gl_static][s] * 8 * cells_rank
             per[s] = (ms, byts)
@@ -234,7 +243,7 @@ def main():
         if os.path.exists(pmc) and not a.wave:
             try:
                 ps = json.load(open(pmc))
-                key = f"stage{dom}_gl{int(a.gl_static)}_{n1}x{n2}x{sim.grid.n3}_m{a.mode}"
+                key = f"{'pair' if pairs else 'stage'}{dom}_gl{int(a.gl_static)}_{n1}x{n2}x{sim.grid.n3}_m{a.mode}"
                 traffic = ps.get(key, {}).get("hbm_bytes_per_launch")
                 if traffic is not None:
                     # not measured in this run: the calibrated FETCH_SIZE + WRITE_SIZE of that
@@ -244,7 +253,7 @@ def main():
                 traffic = None
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": kernel_name(dom, a, rc_path, n1),
+                "kernel": kernel_name(dom, a, rc_path, n1, pairs),
                 "algorithmic_bytes_per_launch": byts // nl[dom],
                 "avg_launch_ms": round(ms / nl[dom], 4),
                 "stages_ms": {str(s): round(per[s][0], 4) for s in per},
@@ -283,11 +292,12 @@ def main():
                    "service_callback": a.callback,
                    "pipeline": ("two-stream" if a.two_stream else "comm-boundary" if a.comm_boundary
                                 else "one-stream"), "wave": a.wave,
-                   "gl_store_skipped": gl_keep,
+                   "gl_store_skipped": gl_keep, "pair_kernels": pairs,
                    "tiles": ({str(k): ("cache" if v[0] == 0 else f"{2 * v[1]}x{v[2]} cells")
                               for k, v in geo.items()} if geo else None)},
         "roofline": roof,
-        # whole step at its algorithmic bytes (39 doubles per cell-step), per GPU
+        # whole step at its algorithmic bytes (21 doubles per cell-step with the pair kernels, 39
+        # with one launch per stage), per GPU
         "step_algorithmic_GBps": round(step_bytes * cells_total * steps / el / 1e9 / world, 1),
         "init_s": round(init_s, 2),
     }
@@ -370,9 +380,11 @@ def wave_launches(n3, w):
     return nl
 
 
-def kernel_name(stage, a, rc_path, n1):
-    """the stage kernel libpft launches for these options (pft_kernels.hip launch_stage)"""
+def kernel_name(stage, a, rc_path, n1, pairs=False):
+    """the stage kernel libpft launches for these options (pft_kernels.hip launch_stage, run_pair)"""
     gls = "true" if a.gl_static else "false"
+    if pairs and stage in (3, 5):
+        return f"merson_pair<{stage - 1}, {a.mode}, {gls}>"
     if a.tile == 0 or n1 % 2:
         return f"merson_stage<{stage}, {a.mode}, {gls}>"
     wx = (16 if stage <= 2 else 32) if a.tile == 1 else a.tile

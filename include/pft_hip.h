@@ -159,6 +159,16 @@ int pft_slab_swap_buffers(pft_slab * s, int a, int b);
 int pft_slab_can_speculate(const pft_slab * s);
 int pft_slab_stage_spec(pft_slab * s, double t_stage, int k_begin, int k_end);
 int pft_slab_eps_mark(pft_slab * s);
+/* Pair kernels (one slab, recompute path): stages 2+3 or 4+5 of the step (first = 2 or 4) in ONE
+   launch.  Stage A's K is evaluated on the tile and a one-cell ring and never stored; stage B
+   writes K3 (first = 2) or the error norm and x(t+h) into XN (first = 4), bit for bit what the
+   two stage launches give.  t_a / t_b: the two stage times (Dirichlet value); h: the step; coef:
+   h3 for x(t+h).  pair_ok: 1 when this slab runs them (even n1, no z-neighbours, not disabled by
+   set_pair(s, 0) or env PFT_PAIR=0); pair_geometry: the tile (tx cells x ty rows) */
+int pft_slab_set_pair(pft_slab * s, int on);
+int pft_slab_pair_ok(const pft_slab * s);
+int pft_slab_pair_geometry(const pft_slab * s, int * tx, int * ty);
+int pft_slab_pair(pft_slab * s, int first, double t_a, double t_b, double h, double coef);
 /* the same publication enqueued on another stream of the slab's device (the communication
    stream, behind the eps max over ranks: pft_comm_eps_publish) */
 int pft_slab_eps_mark_on(pft_slab * s, void * stream);

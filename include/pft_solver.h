@@ -61,10 +61,14 @@ enum {
 	                           z-wavefront of W-plane launches (chunk c: stage s on planes
 	                           [cW - s + 1, (c+1)W - s + 1)), so each K is read back while it is
 	                           still in the Infinity Cache; 0 (default) = one launch per stage */
-	PFT_OPT_LAZY_ALLOC = 9  /* 1: RK_MPI_SA_init only checks its arguments and the device buffers
+	PFT_OPT_LAZY_ALLOC = 9, /* 1: RK_MPI_SA_init only checks its arguments and the device buffers
 	                           are allocated by the first solve (host-only checks of the ABI);
 	                           0 (default): RK_MPI_SA_init allocates them, as hybrid2.c:101-112
 	                           allocates K1..K5 and aux, and returns -1 when that fails */
+	PFT_OPT_PAIR = 10       /* 1 (default): on one slab, stages 2+3 and 4+5 run as pair kernels
+	                           (pft_slab_pair: stage A evaluated inside stage B's stencil, never
+	                           stored -- 21 instead of 39 doubles per cell-step, bit-identical);
+	                           0: one launch per stage */
 };
 int pft_solver_set_option(int opt, long value);
 
@@ -76,6 +80,8 @@ typedef struct {
 	double last_eps;        /* max error norm of the last attempted step */
 	double stage_ms[6];     /* PFT_OPT_TIMING: summed HIP-event time of stages 1..5 */
 	long stage_n[6];        /* number of timed stage executions */
+	int pairs;              /* 1: the last fused call ran stages 2+3 and 4+5 as pair kernels
+	                           (timed as stages 3 and 5) */
 } pft_solver_stats;
 int pft_solver_get_stats(pft_solver_stats * st);
 

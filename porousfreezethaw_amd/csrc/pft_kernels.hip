@@ -1109,6 +1109,405 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT
 }
 
 // ------------------------------------------------------------------------------------------
+// the pair kernel: two consecutive Merson stages (2+3, or 4+5) in ONE z-march.
+//
+// Stage B's input at a cell is a pointwise combine of x, the K's and stage A's K there
+// (hybrid2.c:408 / :449), so stage B's 7-point stencil at the tile needs stage A's K on the tile
+// plus a one-cell ring, and stage A's stencil there needs stage A's input on a two-cell ring.  A
+// workgroup recomputes stage A on its ring (the neighbouring workgroups compute the same cells
+// with the same operands in the same order: the same bits) and never stores it: K2 and K4 do
+// not exist in HBM, and neither stage re-reads x and the K's the other one read.  Per cell-step:
+//   stages 2, 3 apart: (5 + 2) + (5 + 2) = 14 doubles -> pair 2+3: x, K1 in, K3 out = 7
+//   stages 4, 5 apart: (7 + 2) + (9 + 2) = 20 doubles -> pair 4+5: x, K1, K3 in, x(t+h) out = 9
+// so the step (speculative stage 1 + the two pairs) moves 21 instead of 39 doubles per cell.
+//
+// Workgroup (PFT_PBLOCK threads): an R0 tile of tx x ty cells (tx even) is stage B's output.
+// Thread (px, py) holds the cell pair (x0 - 2 + 2 px, x0 - 1 + 2 px) of row y0 - 2 + py, for px
+// in [0, tx/2 + 2) and py in [0, ty + 4): the tile plus a two-cell ring (R2).  Every thread loads
+// its pair's operands and writes stage A's input into LDS (plane ring lA); threads of rows
+// 1..ty+2 (the tile plus a one-cell ring, R1) evaluate stage A at their pair and write stage B's
+// input into LDS (plane ring lB); threads of the tile evaluate stage B.  A position outside the
+// domain (walls) holds the mirror image the reference's ghost fill puts there (equation.c:137-174:
+// ghost -1-m = interior m): its thread loads the mirrored in-domain pair ("acting" pair), stores
+// it into LDS with its halves exchanged when mirrored in x, and evaluates stage A exactly as the
+// acting pair's own thread does -- so the mirrored stage-B input is the reference's bit for bit.
+// z neighbours of both levels are read from the plane rings (own pair: written by the thread
+// itself; x/y neighbours: written one iteration earlier, behind the barrier).
+#ifndef PFT_PBLOCK
+#define PFT_PBLOCK 512
+#endif
+#define PFT_PAIR_PAD 4          // doubles before / after each LDS field plane: the discarded outer
+                                // cell of a ring pair reads one slot beyond its row
+#ifndef PFT_PAIR_LFA
+#define PFT_PAIR_LFA 1024       // (tx + 4)(ty + 4) + 2 pad doubles per field and plane (stage A input)
+#endif
+#ifndef PFT_PAIR_LFB
+#define PFT_PAIR_LFB 936        // (tx + 4)(ty + 2) + 2 pad (stage B input)
+#endif
+// pairs (bit SA) whose stage-B input operands stay in registers instead of being re-loaded
+#ifndef PFT_PAIR_RES_MASK
+#define PFT_PAIR_RES_MASK ((1 << 2) | (1 << 4))
+#endif
+#ifndef PFT_PAIR_SCHED
+#define PFT_PAIR_SCHED 0
+#endif
+#ifndef PFT_PAIR_LATE_MASK
+#define PFT_PAIR_LATE_MASK (1 << 4)
+#endif
+
+struct PairArgs {
+  const double* x;
+  const double* k1;
+  const double* k3;     // pair 4+5 only
+  double* out;          // pair 2+3: K3 (u, p); pair 4+5: x(t+h) (u, p; gl unless gl_keep)
+  const double* noise;  // u_noise [k][j][i] or null
+  unsigned long long* eps_bits;
+  unsigned int* nonfinite;
+  unsigned long long* pub;   // in-kernel publication of the error norm (as merson_fused<5>)
+  unsigned int* pub_count;
+  long fs;
+  int n1, n2, n3, plane;
+  int k_begin, k_end, kz, ntile, nchunk, ntx;
+  int tx, ty;           // R0 tile: tx cells (even) x ty rows
+  double T_topA, T_topB;   // Dirichlet u above the top plane at the two stage times
+  double cinA, cinB;    // stage-input coefficients: h/3, h/6 (2+3); h/8, h (4+5)
+  double coef;          // x(t+h) coefficient h/3 (4+5)
+  double em0, em1, em2;
+  int gl_keep;
+};
+
+// operands of one cell pair: x (u, p, gl), K1 and K3 (u, p; gl's K's are the literal zeros of
+// dgl, equation.c:731,874)
+struct PairRaw {
+  dbl2 x[3], k1[2], k3[2];
+};
+
+// 16-byte load / store at a byte offset from a wave-uniform base: the base stays in SGPRs and the
+// per-lane offset is one 32-bit VGPR for every array (global_load saddr + voffset), instead of a
+// 64-bit address per array and plane (pft_slab_pair_ok: a field is < 4 GiB)
+__device__ __forceinline__ dbl2 ldb(const double* base, unsigned bo)
+{
+  return *reinterpret_cast<const dbl2*>(reinterpret_cast<const char*>(base) + bo);
+}
+__device__ __forceinline__ void stb(double* base, unsigned bo, dbl2 v)
+{
+  *reinterpret_cast<dbl2*>(reinterpret_cast<char*>(base) + bo) = v;
+}
+
+template <int SA>
+__device__ __forceinline__ void pair_load(const PairArgs& a, unsigned bo, PairRaw& r)
+{
+#pragma unroll
+  for (int q = 0; q < 3; ++q) r.x[q] = ldb(a.x + q * a.fs, bo);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    r.k1[q] = ldb(a.k1 + q * a.fs, bo);
+    if (SA == 4) r.k3[q] = ldb(a.k3 + q * a.fs, bo);
+  }
+}
+
+// stage A's input (stage 2: hybrid2.c:388; stage 4: :428) -- the expressions of stage_in
+template <int SA, bool GLS>
+__device__ __forceinline__ dbl2 pair_in_A(const PairArgs& a, int q, const PairRaw& r)
+{
+  if (GLS && q == 2) return r.x[2];
+  constexpr dbl2 z = {0.0, 0.0};
+  const dbl2 k1 = q < 2 ? r.k1[q < 2 ? q : 0] : z;
+  const dbl2 k3 = (SA == 4 && q < 2) ? r.k3[q < 2 ? q : 0] : z;
+  dbl2 v;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    if (SA == 2) v[s] = k1[s] * a.cinA + r.x[q][s];
+    else v[s] = (k1[s] + 3.0 * k3[s]) * a.cinA + r.x[q][s];
+  }
+  return v;
+}
+
+// stage B's input from the operands and stage A's K at the cell (stage 3: (K1 + K2) h/6 + x,
+// hybrid2.c:408; stage 5: (0.5 K1 - 1.5 K3 + 2 K4) h + x, :449)
+template <int SA, bool GLS>
+__device__ __forceinline__ dbl2 pair_in_B(const PairArgs& a, int q, const PairRaw& r, dbl2 KA)
+{
+  if (GLS && q == 2) return r.x[2];
+  constexpr dbl2 z = {0.0, 0.0};
+  const dbl2 k1 = q < 2 ? r.k1[q < 2 ? q : 0] : z;
+  const dbl2 k3 = (SA == 4 && q < 2) ? r.k3[q < 2 ? q : 0] : z;
+  dbl2 v;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    if (SA == 2) v[s] = (k1[s] + KA[s]) * a.cinB + r.x[q][s];
+    else v[s] = (0.5 * k1[s] - 1.5 * k3[s] + 2.0 * KA[s]) * a.cinB + r.x[q][s];
+  }
+  return v;
+}
+
+// a pair from LDS with its halves exchanged when sw = 1 (two 8-byte reads at per-thread offsets)
+__device__ __forceinline__ dbl2 ld2x(const double* p, int sw)
+{
+  dbl2 v;
+  v.x = p[sw];
+  v.y = p[1 - sw];
+  return v;
+}
+
+// the RHS of one cell pair (du, dp of both cells): centre zc, z neighbours zm / zp, x/y
+// neighbours from the LDS plane L at slot lo; the x-face between the pair's cells is evaluated
+// once and the z-face below is carried in fz (rhs_cell_f, bit-exact), as in merson_fused
+template <int MODE>
+__device__ __forceinline__ void pair_rhs(const pft_consts& c, const double* L0, const double* L1, const double* L2,
+                                         int lo, int LW, const dbl2* zm, const dbl2* zc, const dbl2* zp,
+                                         const double* nz, FaceT* fz, double* du, double* dp)
+{
+  constexpr bool FLUX = MODE != 10 && MODE != 11;
+  const double* L[3] = {L0, L1, L2};
+  FaceT fx;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    Col col[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const double cen = zc[q][s];
+      col[q].c = cen;
+      col[q].xm = s == 0 ? L[q][lo - 1] : zc[q][0];
+      col[q].xp = s == 0 ? zc[q][1] : L[q][lo + 2];
+      col[q].ym = L[q][lo - LW + s];
+      col[q].yp = L[q][lo + LW + s];
+      col[q].zm = zm[q][s];
+      col[q].zp = zp[q][s];
+    }
+    const double un = nz ? zc[0][s] + nz[s] : zc[0][s];
+    const FaceT fxm =
+        s == 0 ? face_of(c, col[1].xm, col[2].xm, col[0].xm, col[1].c, col[2].c, col[0].c, FLUX) : fx;
+    FaceT fzp;
+    rhs_cell_f<MODE>(c, col[0], col[1], col[2], un, fxm, fz[s], fx, fzp, du[s], dp[s]);
+    fz[s] = fzp;
+#if PFT_PAIR_SCHED
+    // one cell's stencil at a time: the scheduler would interleave the two cells' loads and
+    // temporaries and run out of registers
+    if (s == 0) __builtin_amdgcn_sched_barrier(0);
+#endif
+  }
+}
+
+template <int SA, int MODE, bool GLS>
+__global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2))) void merson_pair(PairArgs a,
+                                                                                                   pft_consts c)
+{
+  constexpr bool FLUX = MODE != 10 && MODE != 11;
+  constexpr dbl2 zero2 = {0.0, 0.0};
+  __shared__ __attribute__((aligned(16))) double lA[3][3][PFT_PAIR_LFA];
+  __shared__ __attribute__((aligned(16))) double lB[3][3][PFT_PAIR_LFB];
+
+  const int TX = a.tx, TY = a.ty, LW = TX + 4, WP2 = TX / 2 + 2, NPOS = WP2 * (TY + 4);
+  const int lin = xcd_remap(blockIdx.x, a.ntile * a.nchunk);
+  const int tile = lin % a.ntile, chunk = lin / a.ntile;
+  const int x0 = (tile % a.ntx) * TX, y0 = (tile / a.ntx) * TY;
+  // threads beyond the R2 positions shadow the last one (same loads and LDS writes, no stores)
+  const int tt = min((int)threadIdx.x, NPOS - 1);
+  const int px = tt % WP2, py = tt / WP2;
+  const int pi = x0 - 2 + 2 * px, pj = y0 - 2 + py;          // position: first cell, row
+  // acting pair (in the domain): a mirrored position holds its values (x halves exchanged)
+  const int ai = pi < 0 ? 0 : (pi >= a.n1 ? a.n1 - 2 : pi);
+  const int aj = pj < 0 ? 0 : (pj >= a.n2 ? a.n2 - 1 : pj);
+  const int xsw = (pi < 0 || pi >= a.n1) ? 1 : 0;
+  const unsigned apo = (unsigned)(aj * a.n1 + ai);
+  // byte offset of the acting pair in (interior) plane m of a field
+  auto pbo = [&](int m) -> unsigned { return ((unsigned)(m + 1) * (unsigned)a.plane + apo) * 8u; };
+  const int posA = PFT_PAIR_PAD + py * LW + 2 * px;            // this position in lA
+  const int posB = PFT_PAIR_PAD + (py - 1) * LW + 2 * px;      // ... in lB (rows 1..ty+2)
+  const int actA = PFT_PAIR_PAD + (aj - y0 + 2) * LW + (ai - x0 + 2);   // the acting pair in lA
+  const bool isA = py >= 1 && py <= TY + 2;
+  const bool isB = (int)threadIdx.x < NPOS && px >= 1 && px <= TX / 2 && py >= 2 && py <= TY + 1 &&
+                   pi < a.n1 && pj < a.n2;
+
+  const int kb = a.k_begin + chunk * a.kz;
+  const int ke = min(kb + a.kz, a.k_end);
+  const int n3 = a.n3;
+  const int mA0 = kb > 0 ? kb - 1 : 0;                       // stage-A planes [mA0, mA1]
+  const int mA1 = ke < n3 ? ke : n3 - 1;
+  const int mlast = min(mA1 + 1, n3 - 1);                    // last stage-A input plane
+
+  double m = 0.0;
+  bool nf = false;
+  // Operands in registers: those of plane mm + 1 (landed: stage A's input) and mm + 2 (in
+  // flight).  Stage B's input needs plane mm's again: kept (RES, pair 2+3) or re-loaded (pair 4+5,
+  // one plane after its first load: an L2 hit, not HBM traffic); stage B's outputs (4+5) need plane
+  // mm - 1's: re-loaded -- keeping all would hold ~60 doubles per thread and spill.  The re-loads
+  // are issued before the look-ahead load of plane mm + 2, so that waiting for them (vmcnt counts
+  // in order) never waits for the HBM look-ahead.
+  constexpr bool RES = ((PFT_PAIR_RES_MASK >> SA) & 1) != 0;
+  // LATE: the output re-load and the look-ahead are issued after stage A (fewer registers live
+  // during stage A; the look-ahead then has stage B and the barrier to land)
+  constexpr bool LATE = ((PFT_PAIR_LATE_MASK >> SA) & 1) != 0;
+  PairRaw rn, rnn, rcr;
+  dbl2 kao[2] = {zero2, zero2};  // stage A's K (u, p) at plane mm - 1
+  FaceT fzA[2], fzB[2];
+
+  // prologue: stage A's input of planes mA0 - 1 (if any) and mA0 into the ring; operands of mA0
+  // kept, of mA0 + 1 in flight.  (kb >= ke: an empty chunk, which still takes part in the error
+  // norm's workgroup count below)
+  if (kb < ke) {
+    dbl2 ia0[3], iam[3];
+    PairRaw rc;
+    pair_load<SA>(a, pbo(mA0 + 0), rc);
+    if (mA0 > 0) {
+      PairRaw t;
+      pair_load<SA>(a, pbo(mA0 - 1), t);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        iam[q] = pair_in_A<SA, GLS>(a, q, t);
+        st2x(&lA[(mA0 - 1) % 3][q][posA], iam[q], xsw);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      ia0[q] = pair_in_A<SA, GLS>(a, q, rc);
+      st2x(&lA[mA0 % 3][q][posA], ia0[q], xsw);
+      if (mA0 == 0) iam[q] = ia0[q];                         // bottom wall: mirror (equation.c:164-174)
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) fzA[s] = face_of(c, iam[1][s], iam[2][s], iam[0][s], ia0[1][s], ia0[2][s], ia0[0][s], FLUX);
+    if (mA0 + 1 <= mlast) pair_load<SA>(a, pbo(mA0 + 1), rn);
+    if (RES) rcr = rc;
+    __syncthreads();
+  }
+
+  for (int mm = mA0; kb < ke && mm <= ke; ++mm) {
+    const int sA = mm % 3, sAm = (mm + 2) % 3, sAp = (mm + 1) % 3;   // ring slots of planes mm, mm-1, mm+1
+    // stage A's input of plane mm + 1 (own pair: read back by this thread in this iteration; x/y
+    // neighbours: in the next one, behind the barrier)
+    if (mm + 1 <= mlast) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) st2x(&lA[sAp][q][posA], pair_in_A<SA, GLS>(a, q, rn), xsw);
+    }
+    const int kB = mm - 1;                                   // stage B's plane
+    PairRaw rc, ro;
+    if (!RES && mm <= mA1 && isA) pair_load<SA>(a, pbo(mm + 0), rc);   // plane mm again
+    if (RES) rc = rcr;
+    if (!LATE) {
+      if (SA == 4 && kB >= kb && isB) pair_load<SA>(a, pbo(mm - 1), ro);   // plane kB (outputs)
+      if (mm + 2 <= mlast) pair_load<SA>(a, pbo(mm + 2), rnn);      // look-ahead
+    }
+
+    dbl2 ka[2] = {zero2, zero2};
+    if (mm <= mA1 && isA) {
+      // stage A at plane mm, evaluated as the acting pair's thread does
+      dbl2 zc[3], zm[3], zp[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        zc[q] = ld2x(&lA[sA][q][posA], xsw);
+        zm[q] = mm > 0 ? ld2x(&lA[sAm][q][posA], xsw) : zc[q];
+        zp[q] = mm < n3 - 1 ? ld2x(&lA[sAp][q][posA], xsw) : zc[q];
+      }
+      if (mm == n3 - 1) zp[0] = dbl2{a.T_topA, a.T_topA};     // top: Dirichlet u (equation.c:175-183)
+      double du[2], dp[2];
+      const double* nz = a.noise ? a.noise + (long)mm * a.plane + (long)apo : nullptr;
+      pair_rhs<MODE>(c, &lA[sA][0][0], &lA[sA][1][0], &lA[sA][2][0], actA, LW, zm, zc, zp, nz, fzA, du, dp);
+      ka[0] = dbl2{du[0], du[1]};
+      ka[1] = dbl2{dp[0], dp[1]};
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        st2x(&lB[sA][q][posB], pair_in_B<SA, GLS>(a, q, rc, q < 2 ? ka[q < 2 ? q : 0] : zero2), xsw);
+    }
+
+    if (LATE) {
+      if (SA == 4 && kB >= kb && isB) pair_load<SA>(a, pbo(mm - 1), ro);
+      if (mm + 2 <= mlast) pair_load<SA>(a, pbo(mm + 2), rnn);
+    }
+    if (kB >= kb && isB) {
+      const int sB = kB % 3, sBm = (kB + 2) % 3, sBp = mm % 3;
+      const int lo = posB;
+      dbl2 zc[3], zm[3], zp[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        zc[q] = ld2(&lB[sB][q][lo]);
+        zm[q] = kB > 0 ? ld2(&lB[sBm][q][lo]) : zc[q];
+        zp[q] = kB < n3 - 1 ? ld2(&lB[sBp][q][lo]) : zc[q];
+      }
+      if (kB == n3 - 1) zp[0] = dbl2{a.T_topB, a.T_topB};
+      if (kB == kb) {
+        // the z-face below the chunk's first stage-B plane
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          fzB[s] = face_of(c, zm[1][s], zm[2][s], zm[0][s], zc[1][s], zc[2][s], zc[0][s], FLUX);
+      }
+      double du[2], dp[2];
+      const unsigned e0 = pbo(kB);
+      const double* nz = a.noise ? a.noise + (long)kB * a.plane + (long)apo : nullptr;
+      pair_rhs<MODE>(c, &lB[sB][0][0], &lB[sB][1][0], &lB[sB][2][0], lo, LW, zm, zc, zp, nz, fzB, du, dp);
+      if (SA == 2) {
+        stb(a.out, e0, dbl2{du[0], du[1]});                   // K3 (hybrid2.c:412-429)
+        stb(a.out + a.fs, e0, dbl2{dp[0], dp[1]});
+      } else {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          if (GLS && q == 2) continue;
+          const dbl2 K = q == 0 ? dbl2{du[0], du[1]} : (q == 1 ? dbl2{dp[0], dp[1]} : zero2);
+          const dbl2 k1 = q < 2 ? ro.k1[q < 2 ? q : 0] : zero2;
+          const dbl2 k3 = q < 2 ? ro.k3[q < 2 ? q : 0] : zero2;
+          const dbl2 k4 = q < 2 ? kao[q < 2 ? q : 0] : zero2;
+          dbl2 r;
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const double em = q == 0 ? a.em0 : (q == 1 ? a.em1 : a.em2);
+            const double ev = em * fabs(0.2 * k1[s] - 0.9 * k3[s] + 0.8 * k4[s] - 0.1 * K[s]);   // :521
+            if (ev > m) m = ev;                                                            // NaN never wins
+            nf |= !isfinite(ev);
+            r[s] = ro.x[q][s] + a.coef * (0.5 * (k1[s] + K[s]) + 2.0 * k4[s]);            // :667
+          }
+          if (!(q == 2 && a.gl_keep)) stb(a.out + q * a.fs, e0, r);
+        }
+      }
+    }
+    if (mm == ke) break;
+    __syncthreads();
+    if (SA == 4) {
+      kao[0] = ka[0];
+      kao[1] = ka[1];
+    }
+    if (RES) rcr = rn;
+    rn = rnn;
+  }
+
+  if (SA == 4) {
+    __shared__ double red[PFT_PBLOCK / 64];
+    __shared__ int rnf[PFT_PBLOCK / 64];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double ov = __shfl_xor(m, off, 64);
+      if (ov > m) m = ov;
+    }
+    const int anynf = __any(nf);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+      red[w] = m;
+      rnf[w] = anynf;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double bm = red[0];
+      int bnf = rnf[0];
+      for (int q = 1; q < PFT_PBLOCK / 64; ++q) {
+        if (red[q] > bm) bm = red[q];
+        bnf |= rnf[q];
+      }
+      if (bm > 0.0) atomicMax(a.eps_bits, (unsigned long long)__double_as_longlong(bm));
+      if (bnf) atomicOr(a.nonfinite, 1u);
+      if (a.pub) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (atomicAdd(a.pub_count, 1u) == gridDim.x - 1) {
+          const unsigned long long e = atomicExch(a.eps_bits, 0ULL);
+          const unsigned int f = atomicExch(a.nonfinite, 0u);
+          atomicExch(a.pub_count, 0u);
+          __hip_atomic_store(a.pub, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(a.pub + 1, (unsigned long long)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // layout conversion kernels (host padded layout, ghost thickness 2 <-> device layout)
 
 __global__ void publish_kernel(unsigned long long* __restrict__ d, unsigned long long* host)
@@ -1328,6 +1727,7 @@ struct pft_slab {
   int n1_tiled_ok;
   int recompute;         // 1: stage inputs rebuilt from x and the K's (no aux arrays)
   int gl_keep;           // X and XN hold the same gl, and x + c*0.0 == x for every gl value
+  int pair_on;           // 1: stages 2+3 and 4+5 may run as pair kernels (merson_pair)
   // per-stage timing: a ring of begin/end event pairs, so that kernels still running when the
   // host collects (the speculative stage 1) are picked up by a later collect
   hipEvent_t tev[6][PFT_TRING][2];
@@ -1386,6 +1786,9 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
     // push inside the stage kernels 5-9% (its boundary workgroups finish last)
     const char* e = getenv("PFT_IPC_FUSED_PUSH");
     s->fused_push = e ? atoi(e) : 0;
+    // pair kernels where the slab qualifies (pft_slab_pair_ok); env PFT_PAIR=0 turns them off (A/B)
+    const char* ep = getenv("PFT_PAIR");
+    s->pair_on = ep ? atoi(ep) : 1;
   }
   const size_t bytes = sizeof(double) * 3 * (size_t)s->fs;
   hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
@@ -2101,6 +2504,184 @@ int pft_slab_stage_spec(pft_slab* s, double t_stage, int k_begin, int k_end)
   if (slab_kind(s) != KFUSED) return -2;
   return run_stage(s, 1, s->buf[PFT_BUF_XN], s->buf[PFT_BUF_A1], nullptr, t_stage, 0.0, 0.0, k_begin, k_end,
                    s->d.gl_static, KFUSED);
+}
+
+}  // extern "C"
+
+// ---- pair kernels (merson_pair): stages 2+3 and 4+5 of a step, one launch each -------------
+
+template <int SA, bool GLS>
+static void launch_pair_mode(int mode, dim3 g, hipStream_t st, const PairArgs& a, const pft_consts& c)
+{
+  switch (mode) {
+    case 0: merson_pair<SA, 0, GLS><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
+    case 1: merson_pair<SA, 1, GLS><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
+    case 2: merson_pair<SA, 2, GLS><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
+    case 10: merson_pair<SA, 10, GLS><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
+    case 11: merson_pair<SA, 11, GLS><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
+  }
+}
+
+template <int SA, bool GLS>
+static int pair_occupancy_mode(int mode)
+{
+  static int cache[12] = {0};
+  int& n = cache[mode];
+  if (n) return n;
+  const void* f = mode == 0 ? (const void*)merson_pair<SA, 0, GLS>
+                : mode == 1 ? (const void*)merson_pair<SA, 1, GLS>
+                : mode == 2 ? (const void*)merson_pair<SA, 2, GLS>
+                : mode == 10 ? (const void*)merson_pair<SA, 10, GLS>
+                             : (const void*)merson_pair<SA, 11, GLS>;
+  int b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, PFT_PBLOCK, 0) != hipSuccess || b < 1) b = 1;
+  n = b;
+  return n;
+}
+
+// pair tile: tx cells (even) x ty rows; its R2 positions ((tx/2 + 2) pairs x (ty + 4) rows) one
+// per thread, and the two LDS plane rings within their static sizes
+static bool pair_geometry_ok(int tx, int ty)
+{
+  return tx >= 2 && tx % 2 == 0 && ty >= 1 && (tx / 2 + 2) * (ty + 4) <= PFT_PBLOCK &&
+         (tx + 4) * (ty + 4) + 2 * PFT_PAIR_PAD <= PFT_PAIR_LFA &&
+         (tx + 4) * (ty + 2) + 2 * PFT_PAIR_PAD <= PFT_PAIR_LFB;
+}
+
+// automatic tile: the fewest workgroups per plane (a workgroup-plane costs about the same whatever
+// the tile's edge tiles hold), of those the one with the fewest idle tile cells, then the wider.
+// n1 = 200 / 400: 40 x 19 cells (5 x 11 / 10 x 22 tiles, 462 of 512 threads evaluate stage A and
+// 380 stage B).  Returns the tiles per plane, 0 when no tile fits (n1 odd).
+static long pair_geometry(int n1, int n2, int* tx_out, int* ty_out)
+{
+  long best = 0, best_idle = 0;
+  int bx = 0, by = 0;
+  if (n1 < 2 || n1 % 2 || n2 < 1) return 0;
+  for (int tx = 2; tx <= n1 + 1 && tx <= 2 * PFT_PBLOCK; tx += 2) {
+    int ty = std::min(n2, PFT_PBLOCK);
+    while (ty >= 1 && !pair_geometry_ok(tx, ty)) --ty;
+    if (ty < 1) continue;
+    const long nt = (long)((n1 + tx - 1) / tx) * ((n2 + ty - 1) / ty);
+    const long idle = nt * tx * ty - (long)n1 * n2;
+    if (best == 0 || nt < best || (nt == best && idle <= best_idle)) {
+      best = nt;
+      best_idle = idle;
+      bx = tx;
+      by = ty;
+    }
+  }
+  *tx_out = bx;
+  *ty_out = by;
+  return best;
+}
+
+static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, double coef)
+{
+  const int mode = s->d.calc_mode;
+  if (mode != 0 && mode != 1 && mode != 2 && mode != 10 && mode != 11) return -2;
+  if (first != 2 && first != 4) return -2;
+  PairArgs a;
+  memset(&a, 0, sizeof(a));
+  a.x = s->buf[PFT_BUF_X];
+  a.k1 = s->buf[PFT_BUF_K1];
+  a.k3 = s->buf[PFT_BUF_K3];
+  a.out = first == 2 ? s->buf[PFT_BUF_K3] : s->buf[PFT_BUF_XN];
+  a.noise = s->noise;
+  a.eps_bits = s->scratch;
+  a.nonfinite = (unsigned int*)(s->scratch + 1);
+  a.fs = s->fs;
+  a.n1 = s->d.n1;
+  a.n2 = s->d.n2;
+  a.n3 = s->d.n3;
+  a.plane = s->plane;
+  a.k_begin = 0;
+  a.k_end = s->d.n3;
+  if (pair_geometry(a.n1, a.n2, &a.tx, &a.ty) <= 0 || !pair_geometry_ok(a.tx, a.ty)) return -2;
+  a.ntx = (a.n1 + a.tx - 1) / a.tx;
+  a.ntile = a.ntx * ((a.n2 + a.ty - 1) / a.ty);
+  const int nplanes = a.n3;
+  if (s->kz > 0) {
+    a.kz = s->kz;
+  } else {
+    // z-chunks as run_stage's cost model: a chunk of kz planes evaluates stage A on kz + 2 and
+    // loads kz + 3; `occ` workgroups per CU (one: 141 KiB of LDS)
+    const int gls = s->d.gl_static;
+    const int occ = first == 2 ? (gls ? pair_occupancy_mode<2, true>(mode) : pair_occupancy_mode<2, false>(mode))
+                               : (gls ? pair_occupancy_mode<4, true>(mode) : pair_occupancy_mode<4, false>(mode));
+    int best_nch = 1;
+    double best_cost = -1.0;
+    for (int nch = 1; nch <= nplanes; ++nch) {
+      const int kz = (nplanes + nch - 1) / nch;
+      if (nch > 1 && kz == (nplanes + nch - 2) / (nch - 1)) continue;
+      const long nb = (long)a.ntile * ((nplanes + kz - 1) / kz);
+      const long per_cu = (nb + s->n_cu - 1) / s->n_cu;
+      const double rounds = occ <= 2 ? (double)((per_cu + occ - 1) / occ) : std::max(1.0, (double)per_cu / occ);
+      const double cost = rounds * (kz + 2);
+      if (best_cost < 0.0 || cost < 0.95 * best_cost) { best_cost = cost; best_nch = nch; }
+    }
+    a.kz = (nplanes + best_nch - 1) / best_nch;
+  }
+  a.nchunk = (nplanes + a.kz - 1) / a.kz;
+  a.T_topA = t_a < s->c.phase_switch_time ? s->c.top_temp1 : s->c.top_temp2;
+  a.T_topB = t_b < s->c.phase_switch_time ? s->c.top_temp1 : s->c.top_temp2;
+  // exactly the solver's h/3.0, h/6.0 and h/8.0 (and run_stage's stage-input coefficients)
+  a.cinA = first == 2 ? h / 3.0 : h / 8.0;
+  a.cinB = first == 2 ? h / 6.0 : h;
+  a.coef = coef;
+  a.em0 = s->d.eps_mult[0];
+  a.em1 = s->d.eps_mult[1];
+  a.em2 = s->d.eps_mult[2];
+  a.gl_keep = PFT_GL_KEEP && first == 4 && s->gl_keep && std::isfinite(coef) ? 1 : 0;
+  s->pushed_role = -1;
+  s->pub_armed = 0;
+  if (first == 4 && s->inkernel_pub) {
+    const int j = (int)(s->pub_next % PFT_PUB_SLOTS);
+    __atomic_store_n(&s->pub_ring[2 * j], PFT_PUB_SENTINEL, __ATOMIC_RELEASE);
+    __atomic_store_n(&s->pub_ring[2 * j + 1], PFT_PUB_SENTINEL, __ATOMIC_RELEASE);
+    a.pub = s->pub_ring_dev + 2 * j;
+    a.pub_count = s->pub_count;
+    s->pub_armed = 1;
+    s->pub_slot = j;
+  }
+  const dim3 g((unsigned)(a.ntile * a.nchunk));
+  const hipStream_t st = s->stream;
+  if (first == 2) {
+    if (s->d.gl_static) launch_pair_mode<2, true>(mode, g, st, a, s->c);
+    else launch_pair_mode<2, false>(mode, g, st, a, s->c);
+  } else {
+    if (s->d.gl_static) launch_pair_mode<4, true>(mode, g, st, a, s->c);
+    else launch_pair_mode<4, false>(mode, g, st, a, s->c);
+  }
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" {
+
+int pft_slab_set_pair(pft_slab* s, int on)
+{
+  s->pair_on = on ? 1 : 0;
+  return 0;
+}
+
+int pft_slab_pair_ok(const pft_slab* s)
+{
+  int tx, ty;
+  // 32-bit byte offsets within a field (merson_pair's loads and stores)
+  return PFT_GLK_LITERAL && s->pair_on && slab_kind(s) == KFUSED && !s->d.has_below && !s->d.has_above &&
+         (double)s->fs * 8.0 < 4294967296.0 && pair_geometry(s->d.n1, s->d.n2, &tx, &ty) > 0;
+}
+
+int pft_slab_pair_geometry(const pft_slab* s, int* tx, int* ty)
+{
+  *tx = *ty = 0;
+  return pair_geometry(s->d.n1, s->d.n2, tx, ty) > 0 ? 0 : -2;
+}
+
+int pft_slab_pair(pft_slab* s, int first, double t_a, double t_b, double h, double coef)
+{
+  if (!pft_slab_pair_ok(s)) return -2;
+  return run_pair(s, first, t_a, t_b, h, coef);
 }
 
 int pft_slab_swap_buffers(pft_slab* s, int a, int b)

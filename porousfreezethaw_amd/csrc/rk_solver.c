@@ -42,6 +42,7 @@ typedef struct {
 	/* options */
 	int opt_gls, opt_kz, opt_dev, opt_timing, opt_tile, opt_norecompute, opt_one_stream, opt_wave;
 	int opt_lazy;               /* PFT_OPT_LAZY_ALLOC: device buffers at the first solve, not at init */
+	int opt_pair;               /* PFT_OPT_PAIR: stages 2+3 and 4+5 as pair kernels where the slab can */
 	int tstep;                  /* this attempted step's stages are timed (every opt_timing-th) */
 	int last_status;            /* raw status of the last device / communication failure */
 	int in_callback;            /* inside Service_Callback on the fused path (x is on the device) */
@@ -49,7 +50,7 @@ typedef struct {
 } solver_state;
 
 static __thread solver_state R = { .slab_dev = -1, .opt_kz = 0, .opt_dev = -1, .opt_tile = 1,
-                                   .opt_one_stream = 1 };
+                                   .opt_one_stream = 1, .opt_pair = 1 };
 
 static pft_comm * comm(void)
 {
@@ -156,6 +157,7 @@ int pft_solver_set_option(int opt, long value)
 		case PFT_OPT_ONE_STREAM: if(value < 0 || value > 2) return -2; R.opt_one_stream = (int)value; return 0;
 		case PFT_OPT_WAVE: if(value < 0) return -2; R.opt_wave = (int)value; return 0;
 		case PFT_OPT_LAZY_ALLOC: R.opt_lazy = value ? 1 : 0; return 0;
+		case PFT_OPT_PAIR: R.opt_pair = value ? 1 : 0; return 0;
 		case PFT_OPT_RECOMPUTE:
 			R.opt_norecompute = value ? 0 : 1; if(R.slab) pft_slab_set_recompute(R.slab, !R.opt_norecompute); return 0;
 		case PFT_OPT_TILE:
@@ -309,6 +311,18 @@ static int do_stage(int stage, double ts, double coef, double h, long * launches
 	return 0;
 }
 
+/* stages first, first+1 (2+3 or 4+5) of the step as ONE pair kernel (pft_slab_pair; one slab):
+   timed as stage first+1 */
+static int do_pair(int first, double ta, double tb, double h, double coef, long * launches)
+{
+	int rc;
+	if(R.tstep) pft_slab_timing_mark(R.slab, first+1, 0);
+	(*launches)++;
+	rc = pft_slab_pair(R.slab, first, ta, tb, h, coef);
+	if(R.tstep) pft_slab_timing_mark(R.slab, first+1, 1);
+	return rc;
+}
+
 /* PFT_OPT_WAVE = W > 0 (one slab, fused path): the five stages of a step as a skewed z-wavefront
    of W-plane launches.  Chunk c runs stage s on planes [cW - (s-1), (c+1)W - (s-1)), so every
    plane a stage reads from the stage before it (its z+1 neighbour included) was written by an
@@ -379,6 +393,7 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	int nonfinite, rc, ret = 0, to_host = 0;
 	long attempted = 0, launches = 0;
 	int spec, k1_valid = 0;               /* K1 holds f(t, x) for the current t and x */
+	int pair;                             /* stages 2+3 and 4+5 as pair kernels */
 
 	if((rc = ensure_slab())) return rc;
 	pft_slab_set_eps_mult(R.slab, em);
@@ -404,6 +419,9 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	   are unchanged, so the current K1 is still exactly f(t, x) -- the reference recomputes the
 	   same bits (hybrid2.c:373) -- and the speculative one is dropped. */
 	spec = pft_slab_can_speculate(R.slab);
+	/* pair kernels: one slab (no z-neighbours: the stage-A ring would need two ghost planes) */
+	pair = spec && R.opt_pair && R.opt_wave == 0 && !pft_comm_splits(c) && pft_slab_pair_ok(R.slab);
+	R.stats.pairs = pair;
 	/* the error norm goes to the host from stage 5 itself (no publish kernel, no event) where no
 	   device collective sits between stage 5 and the host (one slab, or ipc); env
 	   PFT_INKERNEL_PUBLISH=0 turns it off (A/B) */
@@ -423,6 +441,11 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 		if(R.opt_wave > 0 && spec && !pft_comm_splits(c)) {
 			/* the same five stages as a skewed z-wavefront of W-plane launches (wave_stages) */
 			if((rc = wave_stages(!k1_valid, t, h, h2, h3, h6, h8, &launches))) return rc;
+		} else if(pair) {
+			/* the same arithmetic: stage A of each pair is evaluated inside stage B's stencil */
+			if(!k1_valid && (rc = do_stage(1, t, h3, h, &launches))) return rc;      /* :373-389 */
+			if((rc = do_pair(2, t+h3, t+h3, h, h3, &launches))) return rc;          /* :392-429 */
+			if((rc = do_pair(4, t+h2, t+h, h, h3, &launches))) return rc;           /* :432-524,657-668 */
 		} else {
 			if(!(spec && k1_valid) && (rc = do_stage(1, t, h3, h, &launches))) return rc;  /* :373-389 */
 			if((rc = do_stage(2, t+h3, h6, h, &launches))) return rc;    /* :392-409 */

@@ -1,0 +1,143 @@
+"""Pair kernels (merson_pair, pft_slab_pair): stages 2+3 and 4+5 of the Merson step in one launch
+each, stage A evaluated on the tile plus a one-cell ring inside stage B's z-march and never stored.
+Bit for bit what the five stage launches give (RK_MPI_SAsolver_hybrid2.c:392-524,657-668), on grids
+whose pair tiles fit exactly, leave partial tiles, are one tile wide or narrower than a tile, with
+forced z-chunks (interior chunks recompute stage A on the plane below and above), every calc_mode,
+gl_static, u_noise, and against the oracle and the reference's golden trajectory."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import _oracle as O
+import porousfreezethaw_amd as P
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if P.device_count() < 1:
+        pytest.fail("no HIP device: the gpu tests must run on an MI355X (no CPU fallback exists)")
+
+
+def _run(dims, mode, pair, steps, kz=None, gl_static=False, noise=0.0, tile=2):
+    meta, _ = O.load_case("g20")
+    Pm, info = O.params_from_meta(meta)
+    Pm = Pm.copy()
+    if noise:
+        Pm[O.PARAM_NAMES.index("u_noise_amp")] = noise
+    n1, n2, n3 = dims
+    L = P.lib()
+    L.pft_solver_set_option(P.PFT_OPT_PAIR, 1 if pair else 0)
+    # u_noise comes from the C library's rand() (PrecalculateData, equation.c:450-456): the same
+    # field for both runs
+    C.CDLL("libc.so.6").srand(1)
+    try:
+        sim = P.Simulation(n1, n2, n3, (info["L1"], info["L2"], info["L3"]), mode, Pm, beads=O.beads(),
+                           tau=1.0, tau_min=info["tau_min"], delta=info["delta"], tile=tile, recompute=True,
+                           kz=kz, gl_static=gl_static)
+        ic = sim.interior()
+        rc = sim.solve_ex(1e9, steps, 0)
+        assert rc == 2
+        st = sim.stats()
+        out = (sim.t.hex(), sim.h.hex(), sim.system.steps, sim.system.steps_total, sim.interior())
+        sim.close()
+    finally:
+        L.pft_solver_set_option(P.PFT_OPT_PAIR, 1)
+    assert st.path == 1
+    return out, st.pairs, ic, info, Pm
+
+
+def _same(a, b):
+    assert a[:4] == b[:4]
+    assert np.array_equal(a[4], b[4])
+
+
+# pair tiles (pair_geometry): 30 -> 30 cells wide (one tile), 100x36 -> 34 x 16 ish, 18x12 one
+# tile, 66x38 partial x tile, 252x14 / 318x10 wide planes, 2 x 6 and 4 x 130 narrow ones
+GRIDS = [(30, 30, 60), (100, 36, 40), (18, 12, 30), (66, 38, 21), (252, 14, 6), (318, 10, 5), (2, 6, 5),
+         (4, 130, 9), (50, 50, 100)]
+
+
+@pytest.mark.parametrize("dims", GRIDS)
+@pytest.mark.parametrize("mode", [0, 1, 2, 10, 11])
+def test_pair_equals_stage_kernels(dims, mode):
+    """12 attempted steps (rejections included: h starts at tau = 1 s) with and without pairs"""
+    got, used, *_ = _run(dims, mode, True, 12)
+    ref, unused, *_ = _run(dims, mode, False, 12)
+    assert used == 1 and unused == 0
+    _same(got, ref)
+
+
+@pytest.mark.parametrize("kz", [1, 2, 3, 7])
+@pytest.mark.parametrize("dims", [(30, 30, 60), (66, 38, 21), (2, 6, 5)])
+def test_pair_z_chunks(dims, kz):
+    """forced z-chunks: every chunk but the first recomputes stage A on the plane below its first,
+    every chunk but the last on the plane above its last (one plane per chunk at kz = 1)"""
+    got, used, *_ = _run(dims, 0, True, 8, kz=kz)
+    ref, *_ = _run(dims, 0, False, 8)
+    assert used == 1
+    _same(got, ref)
+
+
+@pytest.mark.parametrize("gl_static", [False, True])
+@pytest.mark.parametrize("noise", [0.0, 0.5])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_pair_gl_static_and_noise(gl_static, noise, mode):
+    """gl read from x (gl_static) and u_noise (equation.c:450-456, 676-687) seen by both stages"""
+    got, used, *_ = _run((66, 38, 21), mode, True, 10, gl_static=gl_static, noise=noise)
+    ref, *_ = _run((66, 38, 21), mode, False, 10, gl_static=gl_static, noise=noise)
+    assert used == 1
+    _same(got, ref)
+
+
+@pytest.mark.parametrize("dims", [(30, 30, 60), (100, 36, 40), (18, 12, 30)])
+def test_pair_matches_oracle(dims):
+    got, used, ic, info, Pm = _run(dims, 0, True, 12)
+    n1, n2, n3 = dims
+    res = O.solve(dict(info, n1=n1, n2=n2, n3=n3), Pm, 0, ic, 0.0, 1.0, [1e9], max_steps_total=12)[0]
+    assert used == 1
+    assert (got[0], got[1], got[2], got[3]) == (res[0].hex(), res[1].hex(), res[2], res[3])
+    assert np.array_equal(got[4], res[5])
+
+
+@pytest.mark.parametrize("mode", [0, 1, 10, 11])
+@pytest.mark.parametrize("gl_static", [False, True])
+def test_pair_golden_trajectory(mode, gl_static):
+    """the reference's own trajectory (g20, 10x10x20) through the pair kernels to every snapshot
+    time, where the golden holds it (modes 0/1); modes 10/11 against the stage kernels"""
+    meta, A = O.load_case("g20")
+    Pm, info = O.params_from_meta(meta)
+    ic = A["traj_m0_ic"] if mode not in (0, 1) else A[f"traj_m{mode}_ic"]
+    runs = {}
+    for pair in (1, 0):
+        P.lib().pft_solver_set_option(P.PFT_OPT_PAIR, pair)
+        sim = P.Simulation(info["n1"], info["n2"], info["n3"], (info["L1"], info["L2"], info["L3"]), mode, Pm,
+                           initial=ic, tau=1.0, tau_min=info["tau_min"], delta=info["delta"], tile=2,
+                           recompute=True, gl_static=gl_static)
+        res = []
+        for T in meta["traj_times"]:
+            rc = sim.solve(T)
+            res.append((sim.t.hex(), sim.h.hex(), sim.system.steps, sim.system.steps_total, rc, sim.interior()))
+        runs[pair] = (res, sim.stats().pairs)
+        sim.close()
+    P.lib().pft_solver_set_option(P.PFT_OPT_PAIR, 1)
+    assert runs[1][1] == 1 and runs[0][1] == 0
+    for a, b in zip(runs[1][0], runs[0][0]):
+        assert a[:5] == b[:5]
+        assert np.array_equal(a[5], b[5])
+    if mode in (0, 1):
+        for i, a in enumerate(runs[1][0]):
+            ref = meta[f"traj_m{mode}"][i]
+            assert a[:5] == (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(), ref[2], ref[3], ref[4])
+            assert np.array_equal(a[5], A[f"traj_m{mode}_state{i}"])
+
+
+def test_pair_full_size_400():
+    """BASELINE configs[1] (200 x 200 x 400, beads): 20 attempted steps with and without pairs, and
+    the pair tile the bench runs (40 x 19 cells)"""
+    got, used, *_ = _run((200, 200, 400), 0, True, 20, tile=1)
+    ref, *_ = _run((200, 200, 400), 0, False, 20, tile=1)
+    assert used == 1
+    _same(got, ref)
