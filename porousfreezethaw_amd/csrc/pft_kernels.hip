@@ -1151,6 +1151,9 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT
 #ifndef PFT_PAIR_SCHED
 #define PFT_PAIR_SCHED 0
 #endif
+#ifndef PFT_PAIR_LATE_LA_MASK
+#define PFT_PAIR_LATE_LA_MASK 0
+#endif
 #ifndef PFT_PAIR_LATE_MASK
 #define PFT_PAIR_LATE_MASK (1 << 4)
 #endif
@@ -1175,6 +1178,44 @@ struct PairArgs {
   double em0, em1, em2;
   int gl_keep;
 };
+// byte offset of the kernel's second argument (pft_consts) in the kernarg segment
+static constexpr unsigned PFT_PAIR_COFF =
+    (unsigned)((sizeof(PairArgs) + alignof(pft_consts) - 1) / alignof(pft_consts) * alignof(pft_consts));
+
+// The z-loop re-reads the kernel arguments (PairArgs, pft_consts) from the kernarg segment with
+// scalar loads at each of its three phases (PFT_PAIR_BIND: the pointer is laundered through an
+// empty asm, so the loads cannot be hoisted out of the loop).  Kept live across the whole loop,
+// the ~25 model constants, the array bases and the step coefficients needed ~190 SGPRs: ~90 were
+// spilled into VGPR lanes and re-read by ~160 v_readlane per iteration.
+// Pairs (bit SA) that do so: pair 4+5 (0.519 -> 0.486 ms at 400^3); pair 2+3, which spilled ~15
+// SGPRs, measured 2% slower with it.
+#ifndef PFT_PAIR_KREL_MASK
+#define PFT_PAIR_KREL_MASK (1 << 4)
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(4))) char* pft_kptr;
+template <bool K>
+__device__ __forceinline__ const PairArgs& pair_bind_a(const PairArgs& a, pft_kptr q)
+{
+  if constexpr (K) return *(const __attribute__((address_space(4))) PairArgs*)q;
+  else return a;
+}
+template <bool K>
+__device__ __forceinline__ const pft_consts& pair_bind_c(const pft_consts& c, pft_kptr q)
+{
+  if constexpr (K) return *(const __attribute__((address_space(4))) pft_consts*)(q + PFT_PAIR_COFF);
+  else return c;
+}
+#define PFT_PAIR_BIND(A, C)                                \
+  pft_kptr kq_##A = kbase;                                \
+  if (KREL) asm volatile("" : "+s"(kq_##A));              \
+  const PairArgs& A = pair_bind_a<KREL>(a, kq_##A);       \
+  const pft_consts& C = pair_bind_c<KREL>(c, kq_##A)
+#else
+#define PFT_PAIR_BIND(A, C) \
+  const PairArgs& A = a;    \
+  const pft_consts& C = c
+#endif
 
 // operands of one cell pair: x (u, p, gl), K1 and K3 (u, p; gl's K's are the literal zeros of
 // dgl, equation.c:731,874)
@@ -1295,6 +1336,10 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
 {
   constexpr bool FLUX = MODE != 10 && MODE != 11;
   constexpr dbl2 zero2 = {0.0, 0.0};
+  constexpr bool KREL = ((PFT_PAIR_KREL_MASK >> SA) & 1) != 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const pft_kptr kbase = (pft_kptr)__builtin_amdgcn_kernarg_segment_ptr();
+#endif
   __shared__ __attribute__((aligned(16))) double lA[3][3][PFT_PAIR_LFA];
   __shared__ __attribute__((aligned(16))) double lB[3][3][PFT_PAIR_LFB];
 
@@ -1339,6 +1384,9 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   // LATE: the output re-load and the look-ahead are issued after stage A (fewer registers live
   // during stage A; the look-ahead then has stage B and the barrier to land)
   constexpr bool LATE = ((PFT_PAIR_LATE_MASK >> SA) & 1) != 0;
+  // LATE_LA: the look-ahead load after stage A as well (else at the top: it then has a whole
+  // iteration to land, and waiting for the output re-load at the end of stage B drains it)
+  constexpr bool LATE_LA = ((PFT_PAIR_LATE_LA_MASK >> SA) & 1) != 0;
   PairRaw rn, rnn, rcr;
   dbl2 kao[2] = {zero2, zero2};  // stage A's K (u, p) at plane mm - 1
   FaceT fzA[2], fzB[2];
@@ -1374,21 +1422,21 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
 
   for (int mm = mA0; kb < ke && mm <= ke; ++mm) {
     const int sA = mm % 3, sAm = (mm + 2) % 3, sAp = (mm + 1) % 3;   // ring slots of planes mm, mm-1, mm+1
+    PFT_PAIR_BIND(A0, C0);
     // stage A's input of plane mm + 1 (own pair: read back by this thread in this iteration; x/y
     // neighbours: in the next one, behind the barrier)
     if (mm + 1 <= mlast) {
 #pragma unroll
-      for (int q = 0; q < 3; ++q) st2x(&lA[sAp][q][posA], pair_in_A<SA, GLS>(a, q, rn), xsw);
+      for (int q = 0; q < 3; ++q) st2x(&lA[sAp][q][posA], pair_in_A<SA, GLS>(A0, q, rn), xsw);
     }
     const int kB = mm - 1;                                   // stage B's plane
     PairRaw rc, ro;
-    if (!RES && mm <= mA1 && isA) pair_load<SA>(a, pbo(mm + 0), rc);   // plane mm again
+    if (!RES && mm <= mA1 && isA) pair_load<SA>(A0, pbo(mm + 0), rc);   // plane mm again
     if (RES) rc = rcr;
-    if (!LATE) {
-      if (SA == 4 && kB >= kb && isB) pair_load<SA>(a, pbo(mm - 1), ro);   // plane kB (outputs)
-      if (mm + 2 <= mlast) pair_load<SA>(a, pbo(mm + 2), rnn);      // look-ahead
-    }
+    if (!LATE && SA == 4 && kB >= kb && isB) pair_load<SA>(A0, pbo(mm - 1), ro);   // plane kB (outputs)
+    if (!LATE_LA && mm + 2 <= mlast) pair_load<SA>(A0, pbo(mm + 2), rnn);          // look-ahead
 
+    PFT_PAIR_BIND(A1, C1);
     dbl2 ka[2] = {zero2, zero2};
     if (mm <= mA1 && isA) {
       // stage A at plane mm, evaluated as the acting pair's thread does
@@ -1399,21 +1447,20 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
         zm[q] = mm > 0 ? ld2x(&lA[sAm][q][posA], xsw) : zc[q];
         zp[q] = mm < n3 - 1 ? ld2x(&lA[sAp][q][posA], xsw) : zc[q];
       }
-      if (mm == n3 - 1) zp[0] = dbl2{a.T_topA, a.T_topA};     // top: Dirichlet u (equation.c:175-183)
+      if (mm == n3 - 1) zp[0] = dbl2{A1.T_topA, A1.T_topA};     // top: Dirichlet u (equation.c:175-183)
       double du[2], dp[2];
-      const double* nz = a.noise ? a.noise + (long)mm * a.plane + (long)apo : nullptr;
-      pair_rhs<MODE>(c, &lA[sA][0][0], &lA[sA][1][0], &lA[sA][2][0], actA, LW, zm, zc, zp, nz, fzA, du, dp);
+      const double* nz = A1.noise ? A1.noise + (long)mm * A1.plane + (long)apo : nullptr;
+      pair_rhs<MODE>(C1, &lA[sA][0][0], &lA[sA][1][0], &lA[sA][2][0], actA, LW, zm, zc, zp, nz, fzA, du, dp);
       ka[0] = dbl2{du[0], du[1]};
       ka[1] = dbl2{dp[0], dp[1]};
 #pragma unroll
       for (int q = 0; q < 3; ++q)
-        st2x(&lB[sA][q][posB], pair_in_B<SA, GLS>(a, q, rc, q < 2 ? ka[q < 2 ? q : 0] : zero2), xsw);
+        st2x(&lB[sA][q][posB], pair_in_B<SA, GLS>(A1, q, rc, q < 2 ? ka[q < 2 ? q : 0] : zero2), xsw);
     }
 
-    if (LATE) {
-      if (SA == 4 && kB >= kb && isB) pair_load<SA>(a, pbo(mm - 1), ro);
-      if (mm + 2 <= mlast) pair_load<SA>(a, pbo(mm + 2), rnn);
-    }
+    PFT_PAIR_BIND(A2, C2);
+    if (LATE && SA == 4 && kB >= kb && isB) pair_load<SA>(A2, pbo(mm - 1), ro);
+    if (LATE_LA && mm + 2 <= mlast) pair_load<SA>(A2, pbo(mm + 2), rnn);
     if (kB >= kb && isB) {
       const int sB = kB % 3, sBm = (kB + 2) % 3, sBp = mm % 3;
       const int lo = posB;
@@ -1424,20 +1471,20 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
         zm[q] = kB > 0 ? ld2(&lB[sBm][q][lo]) : zc[q];
         zp[q] = kB < n3 - 1 ? ld2(&lB[sBp][q][lo]) : zc[q];
       }
-      if (kB == n3 - 1) zp[0] = dbl2{a.T_topB, a.T_topB};
+      if (kB == n3 - 1) zp[0] = dbl2{A2.T_topB, A2.T_topB};
       if (kB == kb) {
         // the z-face below the chunk's first stage-B plane
 #pragma unroll
         for (int s = 0; s < 2; ++s)
-          fzB[s] = face_of(c, zm[1][s], zm[2][s], zm[0][s], zc[1][s], zc[2][s], zc[0][s], FLUX);
+          fzB[s] = face_of(C2, zm[1][s], zm[2][s], zm[0][s], zc[1][s], zc[2][s], zc[0][s], FLUX);
       }
       double du[2], dp[2];
       const unsigned e0 = pbo(kB);
-      const double* nz = a.noise ? a.noise + (long)kB * a.plane + (long)apo : nullptr;
-      pair_rhs<MODE>(c, &lB[sB][0][0], &lB[sB][1][0], &lB[sB][2][0], lo, LW, zm, zc, zp, nz, fzB, du, dp);
+      const double* nz = A2.noise ? A2.noise + (long)kB * A2.plane + (long)apo : nullptr;
+      pair_rhs<MODE>(C2, &lB[sB][0][0], &lB[sB][1][0], &lB[sB][2][0], lo, LW, zm, zc, zp, nz, fzB, du, dp);
       if (SA == 2) {
-        stb(a.out, e0, dbl2{du[0], du[1]});                   // K3 (hybrid2.c:412-429)
-        stb(a.out + a.fs, e0, dbl2{dp[0], dp[1]});
+        stb(A2.out, e0, dbl2{du[0], du[1]});                   // K3 (hybrid2.c:412-429)
+        stb(A2.out + A2.fs, e0, dbl2{dp[0], dp[1]});
       } else {
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
@@ -1449,13 +1496,13 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
           dbl2 r;
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
-            const double em = q == 0 ? a.em0 : (q == 1 ? a.em1 : a.em2);
+            const double em = q == 0 ? A2.em0 : (q == 1 ? A2.em1 : A2.em2);
             const double ev = em * fabs(0.2 * k1[s] - 0.9 * k3[s] + 0.8 * k4[s] - 0.1 * K[s]);   // :521
             if (ev > m) m = ev;                                                            // NaN never wins
             nf |= !isfinite(ev);
-            r[s] = ro.x[q][s] + a.coef * (0.5 * (k1[s] + K[s]) + 2.0 * k4[s]);            // :667
+            r[s] = ro.x[q][s] + A2.coef * (0.5 * (k1[s] + K[s]) + 2.0 * k4[s]);            // :667
           }
-          if (!(q == 2 && a.gl_keep)) stb(a.out + q * a.fs, e0, r);
+          if (!(q == 2 && A2.gl_keep)) stb(A2.out + q * A2.fs, e0, r);
         }
       }
     }
