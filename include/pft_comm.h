@@ -85,6 +85,10 @@ int pft_comm_halo_finish(pft_comm * c);
    later work on the comm stream follows it in stream order */
 int pft_comm_halo_enqueue_comm(pft_comm * c, int buf, int f0, int f1);
 int pft_comm_halo(pft_comm * c, int buf, int f0, int f1);   /* start + finish */
+/* the pair kernels' two-plane halo: planes 1, 2 and n3-1, n3 into the neighbours' ghost and far
+   ghost planes (pft_slab_far), start + finish; needs n3 >= 2 on every slab */
+int pft_comm_halo_deep(pft_comm * c, int buf, int f0, int f1);
+int pft_comm_halo_start_deep(pft_comm * c, int buf, int f0, int f1);   /* ... then pft_comm_halo_finish */
 /* eps max over ranks, on the slab's scratch (u64 bits + non-finite flag), stream-ordered
    (rccl, loopback; a no-op for ipc, whose max is pft_comm_eps_host) */
 int pft_comm_allreduce_eps(pft_comm * c);

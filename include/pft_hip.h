@@ -7,11 +7,13 @@
  * ABI; device buffers are owned by a pft_slab object.  No torch types anywhere.
  *
  * Device layout of one slab (one Z-slab of the reference decomposition, intertrack.c:1776-1800):
- * a "state" is 3 fields (u, p, gl) at stride `fs` doubles; each field holds n3+2 planes of
- * n1*n2 doubles, i fastest: plane 0 is the ghost plane below the slab, planes 1..n3 the
- * interior, plane n3+1 the ghost plane above.  Only ONE ghost plane is kept (the 7-point
- * stencil reads only the first of the reference's two ghost layers, equation.c:659-724);
- * x/y mirror and z-wall conditions are folded into the stencil's index logic.
+ * a "state" is 3 fields (u, p, gl) at stride `fs` doubles; from the buffer pointer a field holds
+ * n3+2 planes of n1*n2 doubles, i fastest: plane 0 is the ghost plane below the slab, planes
+ * 1..n3 the interior, plane n3+1 the ghost plane above.  The stage kernels read only these (the
+ * 7-point stencil reads only the first of the reference's two ghost layers, equation.c:659-724);
+ * the pair kernels also read the far ghost planes -1 and n3+2 (the second layer, exchanged at
+ * slab interfaces only: pft_slab_far).  x/y mirror and z-wall conditions are folded into the
+ * stencil's index logic.
  */
 #ifndef PFT_HIP_H
 #define PFT_HIP_H
@@ -124,6 +126,9 @@ int pft_slab_stage(pft_slab * s, int stage, double t_stage, double coef, double 
                    int k_begin, int k_end);
 /* k_begin value selecting the slab's two boundary planes (0 and n3-1) in one launch */
 #define PFT_K_BOUNDARY (-2)
+/* k_begin value selecting planes 0, 1 and n3-2, n3-1 in one launch (what the z-neighbours' pair
+   kernels read: the two-plane halo) */
+#define PFT_K_BOUNDARY2 (-3)
 
 /* K = f(input) only (RK_RightHandSide semantics), input/output buffer indices */
 int pft_slab_rhs(pft_slab * s, int in_buf, int out_buf, double t);
@@ -163,12 +168,17 @@ int pft_slab_eps_mark(pft_slab * s);
    launch.  Stage A's K is evaluated on the tile and a one-cell ring and never stored; stage B
    writes K3 (first = 2) or the error norm and x(t+h) into XN (first = 4), bit for bit what the
    two stage launches give.  t_a / t_b: the two stage times (Dirichlet value); h: the step; coef:
-   h3 for x(t+h).  pair_ok: 1 when this slab runs them (even n1, no z-neighbours, not disabled by
-   set_pair(s, 0) or env PFT_PAIR=0); pair_geometry: the tile (tx cells x ty rows) */
+   h3 for x(t+h).  set_pair: 0 off, 1 (default) automatic (slabs of >= 16 Ki cells per CU), 2 on
+   any slab they fit; env PFT_PAIR=0/1/2 overrides.  pair_ok: 1 when this slab runs them (even
+   n1, no z-neighbours, the mode allows); pair_geometry: the tile (tx cells x ty rows) */
 int pft_slab_set_pair(pft_slab * s, int on);
 int pft_slab_pair_ok(const pft_slab * s);
 int pft_slab_pair_geometry(const pft_slab * s, int * tx, int * ty);
 int pft_slab_pair(pft_slab * s, int first, double t_a, double t_b, double h, double coef);
+/* the same on planes [k_begin, k_end) (-1/-1: all; k_begin = PFT_K_BOUNDARY2: the two planes at
+   each end, for the N > 1 pipeline that exchanges them beside the interior launch) */
+int pft_slab_pair_range(pft_slab * s, int first, double t_a, double t_b, double h, double coef, int k_begin,
+                        int k_end);
 /* the same publication enqueued on another stream of the slab's device (the communication
    stream, behind the eps max over ranks: pft_comm_eps_publish) */
 int pft_slab_eps_mark_on(pft_slab * s, void * stream);
@@ -210,6 +220,13 @@ int pft_slab_ipc_export(pft_slab * s, void * handles);
 int pft_slab_ipc_set_peer(pft_slab * s, int side, const void * handles, int n3, long fs, int device);
 int pft_slab_ipc_close(pft_slab * s);
 int pft_slab_halo_put(pft_slab * s, int role, int f0, int f1, unsigned long long seq);
+/* the same with deep = 1: also planes 2 and n3-1 into the neighbours' far ghost planes (the pair
+   kernels' two-plane halo) */
+int pft_slab_halo_put2(pft_slab * s, int role, int f0, int f1, int deep, unsigned long long seq);
+/* far ghost plane of buffer `which`, field q: side 0 = two planes below the slab (the neighbour
+   below's plane n3' - 1; plane -1 of the field), side 1 = two above (the neighbour above's plane
+   2; plane n3 + 2) */
+double * pft_slab_far(pft_slab * s, int which, int q, int side);
 /* raise the neighbours' flags to `seq` behind the work on the compute stream (halo_put calls it) */
 int pft_slab_halo_signal(pft_slab * s, unsigned long long seq);
 /* 1 when the last stage launch already stored the boundary planes of buffer `role` into the

@@ -65,10 +65,11 @@ enum {
 	                           are allocated by the first solve (host-only checks of the ABI);
 	                           0 (default): RK_MPI_SA_init allocates them, as hybrid2.c:101-112
 	                           allocates K1..K5 and aux, and returns -1 when that fails */
-	PFT_OPT_PAIR = 10       /* 1 (default): on one slab, stages 2+3 and 4+5 run as pair kernels
-	                           (pft_slab_pair: stage A evaluated inside stage B's stencil, never
-	                           stored -- 21 instead of 39 doubles per cell-step, bit-identical);
-	                           0: one launch per stage */
+	PFT_OPT_PAIR = 10       /* stages 2+3 and 4+5 as pair kernels (pft_slab_pair: stage A evaluated
+	                           inside stage B's stencil, never stored -- 21 instead of 39 doubles
+	                           per cell-step, bit-identical): 1 (default) = on slabs of at least
+	                           16 Ki cells per CU (4 M cells on MI355X), 2 = on any slab they fit,
+	                           0 = one launch per stage */
 };
 int pft_solver_set_option(int opt, long value);
 

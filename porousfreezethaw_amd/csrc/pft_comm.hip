@@ -398,7 +398,7 @@ int pft_comm_attach(pft_comm* c, pft_slab* s)
 
 static void loop_barrier(pft_comm* c) { pthread_barrier_wait(&c->grp->bar); }
 
-static int halo_start(pft_comm* c, int buf, int f0, int f1, bool on_comm)
+static int halo_start(pft_comm* c, int buf, int f0, int f1, bool on_comm, bool deep = false)
 {
   if (!pft_comm_splits(c)) return 0;
   pft_slab* s = c->slab;
@@ -417,7 +417,8 @@ static int halo_start(pft_comm* c, int buf, int f0, int f1, bool on_comm)
     // stream-ordered on the compute stream: put (boundary planes into the neighbours' ghost
     // planes, then their flags), then wait for our own flags
     const unsigned long long seq = ++c->dseq;
-    int rc = pft_slab_take_pushed(s, buf) ? pft_slab_halo_signal(s, seq) : pft_slab_halo_put(s, buf, f0, f1, seq);
+    int rc = (!deep && pft_slab_take_pushed(s, buf)) ? pft_slab_halo_signal(s, seq)
+                                                     : pft_slab_halo_put2(s, buf, f0, f1, deep ? 1 : 0, seq);
     return rc ? rc : pft_slab_halo_wait(s, seq);
   }
   if (c->kind == KIND_RCCL) {
@@ -427,15 +428,25 @@ static int halo_start(pft_comm* c, int buf, int f0, int f1, bool on_comm)
       HCHK(hipStreamWaitEvent(cs, c->ev_ready, 0));
     }
     NCCLCHK(ncclGroupStart());
+    // deep: also the second planes into / from the far ghost planes; per peer the sends and the
+    // peer's receives pair up in the same order (field by field: ghost plane, then far plane)
     for (int f = f0; f < f1; ++f) {
       double* fld = b + f * fs;
       if (below) {
         NCCLCHK(ncclSend(fld + 1 * plane, plane, ncclFloat64, pb, c->nccl, cs));
         NCCLCHK(ncclRecv(fld + 0 * plane, plane, ncclFloat64, pb, c->nccl, cs));
+        if (deep) {
+          NCCLCHK(ncclSend(fld + 2 * plane, plane, ncclFloat64, pb, c->nccl, cs));
+          NCCLCHK(ncclRecv(pft_slab_far(s, buf, f, 0), plane, ncclFloat64, pb, c->nccl, cs));
+        }
       }
       if (above) {
         NCCLCHK(ncclSend(fld + (size_t)n3 * plane, plane, ncclFloat64, pa, c->nccl, cs));
         NCCLCHK(ncclRecv(fld + (size_t)(n3 + 1) * plane, plane, ncclFloat64, pa, c->nccl, cs));
+        if (deep) {
+          NCCLCHK(ncclSend(fld + (size_t)(n3 - 1) * plane, plane, ncclFloat64, pa, c->nccl, cs));
+          NCCLCHK(ncclRecv(pft_slab_far(s, buf, f, 1), plane, ncclFloat64, pa, c->nccl, cs));
+        }
       }
     }
     NCCLCHK(ncclGroupEnd());
@@ -455,11 +466,17 @@ static int halo_start(pft_comm* c, int buf, int f0, int f1, bool on_comm)
       const double* src = pft_slab_buffer(nb, buf) + f * pft_slab_field_stride(nb) +
                           (size_t)pft_slab_nz(nb) * pft_slab_plane(nb);
       HCHK(hipMemcpyAsync(fld, src, plane * sizeof(double), hipMemcpyDeviceToDevice, st));
+      if (deep)
+        HCHK(hipMemcpyAsync(pft_slab_far(s, buf, f, 0), src - pft_slab_plane(nb), plane * sizeof(double),
+                            hipMemcpyDeviceToDevice, st));
     }
     if (above) {
       pft_slab* na = c->grp->slabs[c->rank + 1];
       const double* src = pft_slab_buffer(na, buf) + f * pft_slab_field_stride(na) + pft_slab_plane(na);
       HCHK(hipMemcpyAsync(fld + (size_t)(n3 + 1) * plane, src, plane * sizeof(double), hipMemcpyDeviceToDevice, st));
+      if (deep)
+        HCHK(hipMemcpyAsync(pft_slab_far(s, buf, f, 1), src + pft_slab_plane(na), plane * sizeof(double),
+                            hipMemcpyDeviceToDevice, st));
     }
   }
   HCHK(hipStreamSynchronize(st));
@@ -476,6 +493,14 @@ int pft_comm_halo_finish(pft_comm* c)
   c->pending = 0;
   HCHK(hipStreamWaitEvent((hipStream_t)pft_slab_stream(c->slab), c->ev_done, 0));
   return 0;
+}
+
+int pft_comm_halo_start_deep(pft_comm* c, int buf, int f0, int f1) { return halo_start(c, buf, f0, f1, false, true); }
+
+int pft_comm_halo_deep(pft_comm* c, int buf, int f0, int f1)
+{
+  int rc = halo_start(c, buf, f0, f1, false, true);
+  return rc ? rc : pft_comm_halo_finish(c);
 }
 
 int pft_comm_halo(pft_comm* c, int buf, int f0, int f1)

@@ -9,7 +9,7 @@
 // reference for calc_mode 0/1/10/11 (mode 2 differs only through device cosh, <= 1 ulp).
 //
 // Memory: per slab, a field is (n3+2) planes of n1*n2 doubles (one ghost plane each side, filled
-// only at slab interfaces).  Mirror / Dirichlet walls (equation.c:113-263) are folded into the
+// only at slab interfaces) between two far ghost planes (the pair kernels' two-plane halo).  Mirror / Dirichlet walls (equation.c:113-263) are folded into the
 // neighbour selection: the first mirrored ghost equals the boundary cell itself.
 //
 // Launch geometry: a 256-thread workgroup owns 256 consecutive (i,j) columns of the flattened
@@ -1144,6 +1144,9 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT
 #ifndef PFT_PAIR_LFB
 #define PFT_PAIR_LFB 936        // (tx + 4)(ty + 2) + 2 pad (stage B input)
 #endif
+#ifndef PFT_PAIR_MIN_CELLS_PER_CU
+#define PFT_PAIR_MIN_CELLS_PER_CU 16384
+#endif
 // pairs (bit SA) whose stage-B input operands stay in registers instead of being re-loaded
 #ifndef PFT_PAIR_RES_MASK
 #define PFT_PAIR_RES_MASK ((1 << 2) | (1 << 4))
@@ -1170,7 +1173,10 @@ struct PairArgs {
   unsigned int* pub_count;
   long fs;
   int n1, n2, n3, plane;
+  int has_below, has_above;   // z-neighbours: stage A also runs on the ghost plane next to each,
+                              // from the two-plane halo (ghost + far ghost planes, pft_slab_far)
   int k_begin, k_end, kz, ntile, nchunk, ntx;
+  int kspan;            // planes a chunk runs from its start (kz; 2 for the two-plane boundary launch)
   int tx, ty;           // R0 tile: tx cells (even) x ty rows
   double T_topA, T_topB;   // Dirichlet u above the top plane at the two stage times
   double cinA, cinB;    // stage-input coefficients: h/3, h/6 (2+3); h/8, h (4+5)
@@ -1235,6 +1241,10 @@ __device__ __forceinline__ void stb(double* base, unsigned bo, dbl2 v)
   *reinterpret_cast<dbl2*>(reinterpret_cast<char*>(base) + bo) = v;
 }
 
+// operands of plane m in [-2, n3 + 1] (interior 0..n3-1; -1 and n3 the ghost planes, -2 and n3+1
+// the far ghost planes of the two-plane halo) at byte offset bo = pbo(m).  The PairArgs pointers
+// are the buffers' pointers minus one plane (run_pair): field q holds plane m at q fs + (m + 2)
+// plane from there, so every offset is unsigned.
 template <int SA>
 __device__ __forceinline__ void pair_load(const PairArgs& a, unsigned bo, PairRaw& r)
 {
@@ -1357,7 +1367,9 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   const int xsw = (pi < 0 || pi >= a.n1) ? 1 : 0;
   const unsigned apo = (unsigned)(aj * a.n1 + ai);
   // byte offset of the acting pair in (interior) plane m of a field
-  auto pbo = [&](int m) -> unsigned { return ((unsigned)(m + 1) * (unsigned)a.plane + apo) * 8u; };
+  // byte offset of the acting pair in plane m of a field, from the PairArgs pointers
+  auto pbo = [&](int m) -> unsigned { return ((unsigned)(m + 2) * (unsigned)a.plane + apo) * 8u; };
+  auto slot = [](int p) { return (p + 3) % 3; };             // plane ring slot (p >= -3)
   const int posA = PFT_PAIR_PAD + py * LW + 2 * px;            // this position in lA
   const int posB = PFT_PAIR_PAD + (py - 1) * LW + 2 * px;      // ... in lB (rows 1..ty+2)
   const int actA = PFT_PAIR_PAD + (aj - y0 + 2) * LW + (ai - x0 + 2);   // the acting pair in lA
@@ -1366,11 +1378,15 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
                    pi < a.n1 && pj < a.n2;
 
   const int kb = a.k_begin + chunk * a.kz;
-  const int ke = min(kb + a.kz, a.k_end);
+  const int ke = min(kb + a.kspan, a.k_end);
   const int n3 = a.n3;
-  const int mA0 = kb > 0 ? kb - 1 : 0;                       // stage-A planes [mA0, mA1]
-  const int mA1 = ke < n3 ? ke : n3 - 1;
-  const int mlast = min(mA1 + 1, n3 - 1);                    // last stage-A input plane
+  const bool wlo = !a.has_below, whi = !a.has_above;         // walls (equation.c:164-183)
+  // stage-A planes [mA0, mA1]: the chunk's planes and one on each side -- at a slab interface
+  // the ghost plane (the neighbour's boundary plane, recomputed), at a wall none
+  const int mA0 = kb > 0 ? kb - 1 : (wlo ? 0 : -1);
+  const int mA1 = ke < n3 ? ke : (whi ? n3 - 1 : n3);
+  const int mlast = min(mA1 + 1, whi ? n3 - 1 : n3 + 1);     // last stage-A input plane
+  const int mfirst = wlo ? 0 : -2;                           // first stage-A input plane
 
   double m = 0.0;
   bool nf = false;
@@ -1397,21 +1413,21 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   if (kb < ke) {
     dbl2 ia0[3], iam[3];
     PairRaw rc;
-    pair_load<SA>(a, pbo(mA0 + 0), rc);
-    if (mA0 > 0) {
+    pair_load<SA>(a, pbo(mA0), rc);
+    if (mA0 > mfirst) {
       PairRaw t;
       pair_load<SA>(a, pbo(mA0 - 1), t);
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         iam[q] = pair_in_A<SA, GLS>(a, q, t);
-        st2x(&lA[(mA0 - 1) % 3][q][posA], iam[q], xsw);
+        st2x(&lA[slot(mA0 - 1)][q][posA], iam[q], xsw);
       }
     }
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       ia0[q] = pair_in_A<SA, GLS>(a, q, rc);
-      st2x(&lA[mA0 % 3][q][posA], ia0[q], xsw);
-      if (mA0 == 0) iam[q] = ia0[q];                         // bottom wall: mirror (equation.c:164-174)
+      st2x(&lA[slot(mA0)][q][posA], ia0[q], xsw);
+      if (mA0 == mfirst) iam[q] = ia0[q];                    // bottom wall: mirror (equation.c:164-174)
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) fzA[s] = face_of(c, iam[1][s], iam[2][s], iam[0][s], ia0[1][s], ia0[2][s], ia0[0][s], FLUX);
@@ -1421,7 +1437,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   }
 
   for (int mm = mA0; kb < ke && mm <= ke; ++mm) {
-    const int sA = mm % 3, sAm = (mm + 2) % 3, sAp = (mm + 1) % 3;   // ring slots of planes mm, mm-1, mm+1
+    const int sA = slot(mm), sAm = slot(mm - 1), sAp = slot(mm + 1);   // ring slots of planes mm, mm-1, mm+1
     PFT_PAIR_BIND(A0, C0);
     // stage A's input of plane mm + 1 (own pair: read back by this thread in this iteration; x/y
     // neighbours: in the next one, behind the barrier)
@@ -1431,7 +1447,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
     }
     const int kB = mm - 1;                                   // stage B's plane
     PairRaw rc, ro;
-    if (!RES && mm <= mA1 && isA) pair_load<SA>(A0, pbo(mm + 0), rc);   // plane mm again
+    if (!RES && mm <= mA1 && isA) pair_load<SA>(A0, pbo(mm), rc);   // plane mm again
     if (RES) rc = rcr;
     if (!LATE && SA == 4 && kB >= kb && isB) pair_load<SA>(A0, pbo(mm - 1), ro);   // plane kB (outputs)
     if (!LATE_LA && mm + 2 <= mlast) pair_load<SA>(A0, pbo(mm + 2), rnn);          // look-ahead
@@ -1444,10 +1460,10 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         zc[q] = ld2x(&lA[sA][q][posA], xsw);
-        zm[q] = mm > 0 ? ld2x(&lA[sAm][q][posA], xsw) : zc[q];
-        zp[q] = mm < n3 - 1 ? ld2x(&lA[sAp][q][posA], xsw) : zc[q];
+        zm[q] = (mm > 0 || !wlo) ? ld2x(&lA[sAm][q][posA], xsw) : zc[q];
+        zp[q] = (mm < n3 - 1 || !whi) ? ld2x(&lA[sAp][q][posA], xsw) : zc[q];
       }
-      if (mm == n3 - 1) zp[0] = dbl2{A1.T_topA, A1.T_topA};     // top: Dirichlet u (equation.c:175-183)
+      if (mm == n3 - 1 && whi) zp[0] = dbl2{A1.T_topA, A1.T_topA};     // top: Dirichlet u (equation.c:175-183)
       double du[2], dp[2];
       const double* nz = A1.noise ? A1.noise + (long)mm * A1.plane + (long)apo : nullptr;
       pair_rhs<MODE>(C1, &lA[sA][0][0], &lA[sA][1][0], &lA[sA][2][0], actA, LW, zm, zc, zp, nz, fzA, du, dp);
@@ -1462,16 +1478,16 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
     if (LATE && SA == 4 && kB >= kb && isB) pair_load<SA>(A2, pbo(mm - 1), ro);
     if (LATE_LA && mm + 2 <= mlast) pair_load<SA>(A2, pbo(mm + 2), rnn);
     if (kB >= kb && isB) {
-      const int sB = kB % 3, sBm = (kB + 2) % 3, sBp = mm % 3;
+      const int sB = slot(kB), sBm = slot(kB - 1), sBp = slot(mm);
       const int lo = posB;
       dbl2 zc[3], zm[3], zp[3];
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         zc[q] = ld2(&lB[sB][q][lo]);
-        zm[q] = kB > 0 ? ld2(&lB[sBm][q][lo]) : zc[q];
-        zp[q] = kB < n3 - 1 ? ld2(&lB[sBp][q][lo]) : zc[q];
+        zm[q] = (kB > 0 || !wlo) ? ld2(&lB[sBm][q][lo]) : zc[q];
+        zp[q] = (kB < n3 - 1 || !whi) ? ld2(&lB[sBp][q][lo]) : zc[q];
       }
-      if (kB == n3 - 1) zp[0] = dbl2{A2.T_topB, A2.T_topB};
+      if (kB == n3 - 1 && whi) zp[0] = dbl2{A2.T_topB, A2.T_topB};
       if (kB == kb) {
         // the z-face below the chunk's first stage-B plane
 #pragma unroll
@@ -1672,20 +1688,29 @@ struct PutArgs {
   long dlo_fs;
   double* dhi;                // the neighbour above: its bottom ghost plane (0) of field 0, or null
   long dhi_fs;
+  int deep;                   // 1: also the second planes, into the neighbours' far ghost planes
+  double* flo;                // the neighbour below's far plane above (n3' + 2) of field 0
+  double* fhi;                // the neighbour above's far plane below (-1) of field 0
 };
 
 __global__ __launch_bounds__(256) void halo_put_kernel(PutArgs a)
 {
-  const long n = (long)a.nf * a.plane;   // doubles per side
-  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < 2 * n; e += (long)gridDim.x * blockDim.x) {
-    const bool up = e >= n;
-    const long r = up ? e - n : e;
+  const long n = (long)a.nf * a.plane;   // doubles per side and depth
+  const long tot = (a.deep ? 4 : 2) * n;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
+    const int part = (int)(e / n);       // 0: plane 1 down, 1: plane n3 up, 2: plane 2 down (far), 3: plane n3-1 up (far)
+    const long r = e - part * n;
     const int f = (int)(r / a.plane);
     const long c = r - (long)f * a.plane;
-    if (!up) {
-      if (a.dlo) a.dlo[(a.f0 + f) * a.dlo_fs + c] = a.src[(a.f0 + f) * a.fs + (long)a.plane + c];       // plane 1
+    const int q = a.f0 + f;
+    if (part == 0) {
+      if (a.dlo) a.dlo[q * a.dlo_fs + c] = a.src[q * a.fs + (long)a.plane + c];
+    } else if (part == 1) {
+      if (a.dhi) a.dhi[q * a.dhi_fs + c] = a.src[q * a.fs + (long)a.n3 * a.plane + c];
+    } else if (part == 2) {
+      if (a.flo) a.flo[q * a.dlo_fs + c] = a.src[q * a.fs + 2L * a.plane + c];
     } else {
-      if (a.dhi) a.dhi[(a.f0 + f) * a.dhi_fs + c] = a.src[(a.f0 + f) * a.fs + (long)a.n3 * a.plane + c];  // plane n3
+      if (a.fhi) a.fhi[q * a.dhi_fs + c] = a.src[q * a.fs + (long)(a.n3 - 1) * a.plane + c];
     }
   }
 }
@@ -1774,7 +1799,9 @@ struct pft_slab {
   int n1_tiled_ok;
   int recompute;         // 1: stage inputs rebuilt from x and the K's (no aux arrays)
   int gl_keep;           // X and XN hold the same gl, and x + c*0.0 == x for every gl value
-  int pair_on;           // 1: stages 2+3 and 4+5 may run as pair kernels (merson_pair)
+  int pair_on;           // pair kernels (merson_pair): 0 off, 1 automatic (large slabs), 2 wherever
+                         // they fit (pft_slab_set_pair); env PFT_PAIR overrides
+  int pair_env;          // PFT_PAIR was set
   // per-stage timing: a ring of begin/end event pairs, so that kernels still running when the
   // host collects (the speculative stage 1) are picked up by a later collect
   hipEvent_t tev[6][PFT_TRING][2];
@@ -1817,8 +1844,10 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
   s->d = *d;
   s->c = *c;
   s->plane = d->n1 * d->n2;
-  const long raw = (long)(d->n3 + 2) * s->plane;
-  s->fs = (raw + 63) & ~63L;  // 512-byte aligned field starts
+  // a field: far ghost plane, ghost plane, n3 interior planes, ghost plane, far ghost plane; the
+  // buffer pointer points at the first ghost plane (plane 0 of the kernels' indexing)
+  const long raw = (long)(d->n3 + 4) * s->plane;
+  s->fs = (raw + 63) & ~63L;  // 512-byte aligned field strides
   s->S = (long)(d->n1 + 4) * (d->n2 + 4) * (d->n3 + 4);
   s->kz = 0;
   s->tile_wx = 1;
@@ -1835,9 +1864,10 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
     s->fused_push = e ? atoi(e) : 0;
     // pair kernels where the slab qualifies (pft_slab_pair_ok); env PFT_PAIR=0 turns them off (A/B)
     const char* ep = getenv("PFT_PAIR");
+    s->pair_env = ep != nullptr;
     s->pair_on = ep ? atoi(ep) : 1;
   }
-  const size_t bytes = sizeof(double) * 3 * (size_t)s->fs;
+  const size_t bytes = sizeof(double) * (3 * (size_t)s->fs + 2 * (size_t)s->plane);
   hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
 #if PFT_COMM_HIPRIO
   // the halo exchange's stream at the greatest priority: its RCCL kernel is dispatched ahead of
@@ -1868,12 +1898,12 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
   if (e == hipSuccess) e = hipExtMallocWithFlags((void**)&s->sig, 4096, hipDeviceMallocUncached);
   if (e == hipSuccess) e = hipMemsetAsync(s->sig, 0, 4096, s->stream);
   for (int b = 0; b < PFT_BUF_COUNT && e == hipSuccess; ++b) {
-    e = hipMalloc((void**)&s->buf[b], bytes);
-    s->buf0[b] = s->buf[b];
+    e = hipMalloc((void**)&s->buf0[b], bytes);
+    s->buf[b] = s->buf0[b] + s->plane;   // past the first field's far ghost plane
     s->phys[b] = b;
     // zero-fill on the slab's own stream: the compute stream is non-blocking, so a fill on the
     // null stream would not be ordered before the first upload/kernel (it raced with them)
-    if (e == hipSuccess) e = hipMemsetAsync(s->buf[b], 0, bytes, s->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(s->buf0[b], 0, bytes, s->stream);
   }
   if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
   int dev = 0;
@@ -2171,7 +2201,8 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   if (mode != 0 && mode != 1 && mode != 2 && mode != 10 && mode != 11) return -2;
   // k_begin == PFT_K_BOUNDARY: the slab's two boundary planes (0 and n3 - 1) in ONE launch, two
   // one-plane chunks n3 - 1 planes apart (what the z-neighbours need first)
-  const bool bnd = k_begin == PFT_K_BOUNDARY;
+  const bool bnd = k_begin == PFT_K_BOUNDARY || k_begin == PFT_K_BOUNDARY2;
+  const int bdepth = k_begin == PFT_K_BOUNDARY2 ? 2 : 1;   // PFT_K_BOUNDARY2: planes 0, 1 and n3-2, n3-1
   if (bnd) {
     k_begin = 0;
     k_end = s->d.n3;
@@ -2252,9 +2283,9 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   a.nchunk = (nplanes + a.kz - 1) / a.kz;
   a.kspan = a.kz;
   if (bnd) {
-    a.kz = std::max(1, s->d.n3 - 1);
-    a.kspan = 1;
-    a.nchunk = s->d.n3 > 1 ? 2 : 1;
+    a.kz = std::max(1, s->d.n3 - bdepth);
+    a.kspan = bdepth;
+    a.nchunk = s->d.n3 > bdepth ? 2 : 1;
   }
   a.T_top = t_stage < s->c.phase_switch_time ? s->c.top_temp1 : s->c.top_temp2;
   a.coef = coef;
@@ -2622,17 +2653,19 @@ static long pair_geometry(int n1, int n2, int* tx_out, int* ty_out)
   return best;
 }
 
-static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, double coef)
+static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, double coef, int k_begin,
+                    int k_end)
 {
   const int mode = s->d.calc_mode;
   if (mode != 0 && mode != 1 && mode != 2 && mode != 10 && mode != 11) return -2;
   if (first != 2 && first != 4) return -2;
   PairArgs a;
   memset(&a, 0, sizeof(a));
-  a.x = s->buf[PFT_BUF_X];
-  a.k1 = s->buf[PFT_BUF_K1];
-  a.k3 = s->buf[PFT_BUF_K3];
-  a.out = first == 2 ? s->buf[PFT_BUF_K3] : s->buf[PFT_BUF_XN];
+  // the buffers' pointers minus one plane: the far ghost plane below the first field (pair_load)
+  a.x = s->buf[PFT_BUF_X] - s->plane;
+  a.k1 = s->buf[PFT_BUF_K1] - s->plane;
+  a.k3 = s->buf[PFT_BUF_K3] - s->plane;
+  a.out = (first == 2 ? s->buf[PFT_BUF_K3] : s->buf[PFT_BUF_XN]) - s->plane;
   a.noise = s->noise;
   a.eps_bits = s->scratch;
   a.nonfinite = (unsigned int*)(s->scratch + 1);
@@ -2641,12 +2674,19 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
   a.n2 = s->d.n2;
   a.n3 = s->d.n3;
   a.plane = s->plane;
-  a.k_begin = 0;
-  a.k_end = s->d.n3;
+  a.has_below = s->d.has_below;
+  a.has_above = s->d.has_above;
+  // k_begin == PFT_K_BOUNDARY2: planes 0, 1 and n3-2, n3-1 in one launch (two 2-plane chunks)
+  const bool bnd = k_begin == PFT_K_BOUNDARY2;
+  if (bnd || k_begin < 0) k_begin = 0;
+  if (bnd || k_end < 0 || k_end > s->d.n3) k_end = s->d.n3;
+  if (k_end <= k_begin) return 0;
+  a.k_begin = k_begin;
+  a.k_end = k_end;
   if (pair_geometry(a.n1, a.n2, &a.tx, &a.ty) <= 0 || !pair_geometry_ok(a.tx, a.ty)) return -2;
   a.ntx = (a.n1 + a.tx - 1) / a.tx;
   a.ntile = a.ntx * ((a.n2 + a.ty - 1) / a.ty);
-  const int nplanes = a.n3;
+  const int nplanes = k_end - k_begin;
   if (s->kz > 0) {
     a.kz = s->kz;
   } else {
@@ -2669,6 +2709,12 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
     a.kz = (nplanes + best_nch - 1) / best_nch;
   }
   a.nchunk = (nplanes + a.kz - 1) / a.kz;
+  a.kspan = a.kz;
+  if (bnd) {
+    a.kz = std::max(1, s->d.n3 - 2);
+    a.kspan = 2;
+    a.nchunk = s->d.n3 > 2 ? 2 : 1;
+  }
   a.T_topA = t_a < s->c.phase_switch_time ? s->c.top_temp1 : s->c.top_temp2;
   a.T_topB = t_b < s->c.phase_switch_time ? s->c.top_temp1 : s->c.top_temp2;
   // exactly the solver's h/3.0, h/6.0 and h/8.0 (and run_stage's stage-input coefficients)
@@ -2681,7 +2727,7 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
   a.gl_keep = PFT_GL_KEEP && first == 4 && s->gl_keep && std::isfinite(coef) ? 1 : 0;
   s->pushed_role = -1;
   s->pub_armed = 0;
-  if (first == 4 && s->inkernel_pub) {
+  if (first == 4 && s->inkernel_pub && !bnd && k_begin == 0 && k_end == s->d.n3) {
     const int j = (int)(s->pub_next % PFT_PUB_SLOTS);
     __atomic_store_n(&s->pub_ring[2 * j], PFT_PUB_SENTINEL, __ATOMIC_RELEASE);
     __atomic_store_n(&s->pub_ring[2 * j + 1], PFT_PUB_SENTINEL, __ATOMIC_RELEASE);
@@ -2707,7 +2753,8 @@ extern "C" {
 
 int pft_slab_set_pair(pft_slab* s, int on)
 {
-  s->pair_on = on ? 1 : 0;
+  if (on < 0 || on > 2) return -2;
+  if (!s->pair_env) s->pair_on = on;
   return 0;
 }
 
@@ -2715,7 +2762,16 @@ int pft_slab_pair_ok(const pft_slab* s)
 {
   int tx, ty;
   // 32-bit byte offsets within a field (merson_pair's loads and stores)
-  return PFT_GLK_LITERAL && s->pair_on && slab_kind(s) == KFUSED && !s->d.has_below && !s->d.has_above &&
+  // automatic: slabs of at least PFT_PAIR_MIN_CELLS_PER_CU cells per CU.  Measured (A/B, one box):
+  // 400^3 +14%, the 800^3 8-way rank slab +12%, the 64 M-cell cube +18%, but 200^3 (2 M cells)
+  // -3.5% and 100^3 -4.5%, where the chunks' extra stage-A planes and the launch latency of
+  // fewer, longer workgroups dominate
+  if (s->pair_on == 1 && (double)s->plane * s->d.n3 < (double)s->n_cu * PFT_PAIR_MIN_CELLS_PER_CU) return 0;
+  // z-neighbours: the two-plane halo (pft_comm_halo_deep) needs n3 >= 2, and stage A on a ghost
+  // plane would need the neighbour's u_noise there (not exchanged: one launch per stage then)
+  const bool nb = s->d.has_below || s->d.has_above;
+  if (nb && (s->d.n3 < 2 || s->noise)) return 0;
+  return PFT_GLK_LITERAL && s->pair_on && slab_kind(s) == KFUSED &&
          (double)s->fs * 8.0 < 4294967296.0 && pair_geometry(s->d.n1, s->d.n2, &tx, &ty) > 0;
 }
 
@@ -2727,8 +2783,14 @@ int pft_slab_pair_geometry(const pft_slab* s, int* tx, int* ty)
 
 int pft_slab_pair(pft_slab* s, int first, double t_a, double t_b, double h, double coef)
 {
+  return pft_slab_pair_range(s, first, t_a, t_b, h, coef, -1, -1);
+}
+
+int pft_slab_pair_range(pft_slab* s, int first, double t_a, double t_b, double h, double coef, int k_begin,
+                        int k_end)
+{
   if (!pft_slab_pair_ok(s)) return -2;
-  return run_pair(s, first, t_a, t_b, h, coef);
+  return run_pair(s, first, t_a, t_b, h, coef, k_begin, k_end);
 }
 
 int pft_slab_swap_buffers(pft_slab* s, int a, int b)
@@ -2761,7 +2823,7 @@ int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, lo
   if (!handles) {
     // self exchange (diagnostic, one slab): the planes land in the slab's own ghost planes, which a
     // single slab never reads (mirror bottom, Dirichlet top)
-    for (int b = 0; b < PFT_BUF_COUNT; ++b) p.base[b] = s->buf0[b];
+    for (int b = 0; b < PFT_BUF_COUNT; ++b) p.base[b] = s->buf0[b] + s->plane;
     p.sig = s->sig;
     p.n3 = s->d.n3;
     p.fs = s->fs;
@@ -2774,10 +2836,10 @@ int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, lo
     void* ptr = nullptr;
     const hipError_t e = hipIpcOpenMemHandle(&ptr, h[b], hipIpcMemLazyEnablePeerAccess);
     if (e != hipSuccess) {
-      for (int q = 0; q < b; ++q) (void)hipIpcCloseMemHandle(p.base[q]);
+      for (int q = 0; q < b; ++q) (void)hipIpcCloseMemHandle(p.base[q] - s->plane);
       return fail(e, "hipIpcOpenMemHandle");
     }
-    if (b < PFT_BUF_COUNT) p.base[b] = (double*)ptr;
+    if (b < PFT_BUF_COUNT) p.base[b] = (double*)ptr + s->plane;   // the neighbour's buffer pointer
     else p.sig = (unsigned long long*)ptr;
   }
   p.n3 = n3;
@@ -2795,7 +2857,7 @@ int pft_slab_ipc_close(pft_slab* s)
   for (int side = 0; side < 2; ++side) {
     SlabPeer& p = s->peer[side];
     if (p.on && p.opened) {
-      for (int b = 0; b < PFT_BUF_COUNT; ++b) (void)hipIpcCloseMemHandle(p.base[b]);
+      for (int b = 0; b < PFT_BUF_COUNT; ++b) (void)hipIpcCloseMemHandle(p.base[b] - s->plane);
       (void)hipIpcCloseMemHandle(p.sig);
     }
     memset(&p, 0, sizeof(p));
@@ -2804,6 +2866,17 @@ int pft_slab_ipc_close(pft_slab* s)
 }
 
 int pft_slab_halo_put(pft_slab* s, int role, int f0, int f1, unsigned long long seq)
+{
+  return pft_slab_halo_put2(s, role, f0, f1, 0, seq);
+}
+
+double* pft_slab_far(pft_slab* s, int which, int q, int side)
+{
+  if (which < 0 || which >= PFT_BUF_COUNT || q < 0 || q > 2 || side < 0 || side > 1) return nullptr;
+  return s->buf[which] + q * s->fs + (side ? (long)(s->d.n3 + 2) * s->plane : -(long)s->plane);
+}
+
+int pft_slab_halo_put2(pft_slab* s, int role, int f0, int f1, int deep, unsigned long long seq)
 {
   if (role < 0 || role >= PFT_BUF_COUNT || f0 < 0 || f1 > 3 || f1 <= f0) return -2;
   const int ph = s->phys[role];
@@ -2824,7 +2897,13 @@ int pft_slab_halo_put(pft_slab* s, int role, int f0, int f1, unsigned long long 
     a.dhi_fs = s->peer[1].fs;
   }
   if (!a.dlo && !a.dhi) return 0;
-  const long n = 2L * a.nf * s->plane;
+  if (deep) {
+    // the second boundary planes into the neighbours' far ghost planes (pft_slab_far layout)
+    a.deep = 1;
+    if (s->peer[0].on) a.flo = s->peer[0].base[ph] + (long)(s->peer[0].n3 + 2) * s->plane;
+    if (s->peer[1].on) a.fhi = s->peer[1].base[ph] - (long)s->plane;
+  }
+  const long n = (deep ? 4L : 2L) * a.nf * s->plane;
   const int blocks = (int)std::min<long>(1024, std::max<long>(1, (n + 255) / 256));
   halo_put_kernel<<<blocks, 256, 0, s->stream>>>(a);
   HIPCHK(hipGetLastError());

@@ -43,6 +43,9 @@ typedef struct {
 	int opt_gls, opt_kz, opt_dev, opt_timing, opt_tile, opt_norecompute, opt_one_stream, opt_wave;
 	int opt_lazy;               /* PFT_OPT_LAZY_ALLOC: device buffers at the first solve, not at init */
 	int opt_pair;               /* PFT_OPT_PAIR: stages 2+3 and 4+5 as pair kernels where the slab can */
+	int deep;                   /* this call runs the pair kernels on z-neighbouring slabs: every stage
+	                               launch covers the whole slab and is followed by the two-plane halo
+	                               exchange of its output (pft_comm_halo_deep) */
 	int tstep;                  /* this attempted step's stages are timed (every opt_timing-th) */
 	int last_status;            /* raw status of the last device / communication failure */
 	int in_callback;            /* inside Service_Callback on the fused path (x is on the device) */
@@ -157,7 +160,7 @@ int pft_solver_set_option(int opt, long value)
 		case PFT_OPT_ONE_STREAM: if(value < 0 || value > 2) return -2; R.opt_one_stream = (int)value; return 0;
 		case PFT_OPT_WAVE: if(value < 0) return -2; R.opt_wave = (int)value; return 0;
 		case PFT_OPT_LAZY_ALLOC: R.opt_lazy = value ? 1 : 0; return 0;
-		case PFT_OPT_PAIR: R.opt_pair = value ? 1 : 0; return 0;
+		case PFT_OPT_PAIR: if(value < 0 || value > 2) return -2; R.opt_pair = (int)value; return 0;
 		case PFT_OPT_RECOMPUTE:
 			R.opt_norecompute = value ? 0 : 1; if(R.slab) pft_slab_set_recompute(R.slab, !R.opt_norecompute); return 0;
 		case PFT_OPT_TILE:
@@ -246,6 +249,24 @@ static int do_stage(int stage, double ts, double coef, double h, long * launches
 	const int tstage = stage == 6 ? 1 : stage;
 	int rc, n3;
 	if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 0);
+	if(R.deep) {
+		/* pair path between slabs: the output's two-plane halo (the next pair kernel evaluates its
+		   stage A on the ghost planes too).  RCCL: the two planes at each end first, their exchange
+		   on the comm stream beside the interior launch; ipc: the whole slab, then the put. */
+		n3 = R.slab_grid.n3;
+		if(!pft_comm_device_halo(c) && n3 >= 5) {
+			if((rc = run1(stage, ts, coef, h, PFT_K_BOUNDARY2, 0))) return rc;
+			if((rc = pft_comm_halo_start_deep(c, out_buf, 0, nfields))) return rc;
+			if((rc = run1(stage, ts, coef, h, 2, n3-2))) return rc;
+			if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
+			*launches += 2;
+			return pft_comm_halo_finish(c);
+		}
+		(*launches)++;
+		if((rc = run1(stage, ts, coef, h, -1, -1))) return rc;
+		if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
+		return pft_comm_halo_deep(c, out_buf, 0, nfields);
+	}
 	if(pft_comm_device_halo(c)) {
 		/* ipc: the whole slab in one launch, then (stream-ordered) the boundary planes into the
 		   neighbours' ghost planes and the wait for theirs in ours */
@@ -315,12 +336,27 @@ static int do_stage(int stage, double ts, double coef, double h, long * launches
    timed as stage first+1 */
 static int do_pair(int first, double ta, double tb, double h, double coef, long * launches)
 {
+	pft_comm * c = comm();
+	const int out_buf = first == 2 ? PFT_BUF_K3 : PFT_BUF_XN, n3 = R.slab_grid.n3;
 	int rc;
 	if(R.tstep) pft_slab_timing_mark(R.slab, first+1, 0);
+	if(R.deep && !pft_comm_device_halo(c) && n3 >= 5) {
+		/* between slabs over RCCL: the two planes at each end first, their exchange (K3, or x(t+h):
+		   gl only where stored) beside the interior launch, which reads no ghost plane */
+		const int nf = pft_slab_stage_fields(R.slab, first+1);
+		*launches += 2;
+		if((rc = pft_slab_pair_range(R.slab, first, ta, tb, h, coef, PFT_K_BOUNDARY2, 0))) return rc;
+		if((rc = pft_comm_halo_start_deep(c, out_buf, 0, nf))) return rc;
+		if((rc = pft_slab_pair_range(R.slab, first, ta, tb, h, coef, 2, n3-2))) return rc;
+		if(R.tstep) pft_slab_timing_mark(R.slab, first+1, 1);
+		return pft_comm_halo_finish(c);
+	}
 	(*launches)++;
 	rc = pft_slab_pair(R.slab, first, ta, tb, h, coef);
 	if(R.tstep) pft_slab_timing_mark(R.slab, first+1, 1);
-	return rc;
+	if(rc || !R.deep) return rc;
+	/* between slabs (ipc): the whole slab, then the two-plane halo */
+	return pft_comm_halo_deep(c, out_buf, 0, pft_slab_stage_fields(R.slab, first+1));
 }
 
 /* PFT_OPT_WAVE = W > 0 (one slab, fused path): the five stages of a step as a skewed z-wavefront
@@ -397,6 +433,23 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 
 	if((rc = ensure_slab())) return rc;
 	pft_slab_set_eps_mult(R.slab, em);
+	/* The next step's K1 is computed speculatively right after stage 5 (recompute path): the
+	   kernel runs while the host reads the error norm and decides, so the GPU does not idle
+	   between steps.  Accepted: it is f(t+h, x(t+h)), exactly the next stage 1.  Rejected: x and t
+	   are unchanged, so the current K1 is still exactly f(t, x) -- the reference recomputes the
+	   same bits (hybrid2.c:373) -- and the speculative one is dropped. */
+	spec = pft_slab_can_speculate(R.slab);
+	/* pair kernels (pft_slab_pair_ok: slab size, n3 >= 2 and no u_noise between slabs); every rank
+	   must take the same path -- the exchanges differ */
+	pft_slab_set_pair(R.slab, R.opt_pair);
+	pair = spec && R.opt_wave == 0 && pft_slab_pair_ok(R.slab);
+	if(nprocs > 1) {
+		long long no = !pair;
+		if((rc = pft_comm_allreduce_max_i64(c, &no))) return rc;
+		pair = !no;
+	}
+	R.deep = pair && pft_comm_splits(c);
+	R.stats.pairs = pair;
 	if(!(flags & PFT_SOLVE_REUSE_DEVICE) || !R.device_valid) {
 		if((rc = pft_slab_upload_host(R.slab, PFT_BUF_X, system->x))) return rc;
 		if((rc = pft_slab_upload_host(R.slab, PFT_BUF_XN, system->x))) return rc;
@@ -406,22 +459,19 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 			if(nprocs > 1 && (rc = pft_comm_allreduce_max_i64(c, &unclean))) return rc;
 			pft_slab_set_gl_keep(R.slab, !unclean);
 		}
-		if(nprocs > 1) {
+		if(nprocs > 1 && !R.deep) {
 			if((rc = pft_comm_halo(c, PFT_BUF_X, 0, 3))) return rc;
 			if((rc = pft_comm_halo(c, PFT_BUF_XN, 0, 3))) return rc;
 		}
 	}
+	if(R.deep) {
+		/* two planes deep, also when x stayed on the device (the previous call may have run one
+		   launch per stage, which keeps only the first ghost plane current) */
+		if((rc = pft_comm_halo_deep(c, PFT_BUF_X, 0, 3))) return rc;
+		if((rc = pft_comm_halo_deep(c, PFT_BUF_XN, 0, 3))) return rc;
+	}
 	R.device_valid = 0;
 	R.stats.path = 1;
-	/* The next step's K1 is computed speculatively right after stage 5 (recompute path): the
-	   kernel runs while the host reads the error norm and decides, so the GPU does not idle
-	   between steps.  Accepted: it is f(t+h, x(t+h)), exactly the next stage 1.  Rejected: x and t
-	   are unchanged, so the current K1 is still exactly f(t, x) -- the reference recomputes the
-	   same bits (hybrid2.c:373) -- and the speculative one is dropped. */
-	spec = pft_slab_can_speculate(R.slab);
-	/* pair kernels: one slab (no z-neighbours: the stage-A ring would need two ghost planes) */
-	pair = spec && R.opt_pair && R.opt_wave == 0 && !pft_comm_splits(c) && pft_slab_pair_ok(R.slab);
-	R.stats.pairs = pair;
 	/* the error norm goes to the host from stage 5 itself (no publish kernel, no event) where no
 	   device collective sits between stage 5 and the host (one slab, or ipc); env
 	   PFT_INKERNEL_PUBLISH=0 turns it off (A/B) */

@@ -5,7 +5,8 @@ GPU -- with:
     python tests/_ipc_worker.py <spec.json> <rank>
 
 spec: {"nranks", "shm", "case": "g20" | "default", "grid_nodes", "mode", "times": [...],
-       "steps": max attempted steps per call (0 = none), "out": output prefix, "tile", "self_x"}
+       "steps": max attempted steps per call (0 = none), "out": output prefix, "tile", "self_x",
+       "pair": PFT_OPT_PAIR (default 1: automatic)}
 Writes <out>.<rank>.npz: per call (t, h, steps, steps_total, rc) and this slab's interior."""
 import json
 import os
@@ -28,6 +29,7 @@ def main():
     comm = P.comm_init_ipc(n, rank, spec["shm"], spec.get("device", 0))
     if spec.get("self_x"):
         assert P.lib().pft_comm_set_self_exchange(comm, 1) == 0
+    P.lib().pft_solver_set_option(P.PFT_OPT_PAIR, spec.get("pair", 1))
     if spec["case"] == "g20":
         meta, A = O.load_case("g20")
         Pm, info = O.params_from_meta(meta)
@@ -54,7 +56,8 @@ def main():
     sim.close()
     P.comm_destroy(comm)
     np.savez(f"{spec['out']}.{rank}.npz", rows=np.array(rows), states=np.array(states),
-             path=st.path, launches=st.kernel_launches, first_row=sim.grid.first_row, n3=sim.grid.n3)
+             path=st.path, launches=st.kernel_launches, first_row=sim.grid.first_row, n3=sim.grid.n3,
+             pairs=st.pairs)
 
 
 if __name__ == "__main__":

@@ -78,6 +78,25 @@ def test_g20_processes_equal_reference(tmp_path, nranks, tile, push):
         assert np.array_equal(full, A[f"traj_m0_state{i}"])
 
 
+@pytest.mark.parametrize("nranks,tile,pair", [(2, 2, 2), (3, 2, 2), (4, 32, 2)])
+def test_g20_processes_pair_kernels_equal_reference(tmp_path, nranks, tile, pair):
+    """the pair kernels between processes (PFT_OPT_PAIR 2): stage A also on the ghost planes, from
+    the two-plane halo exchanged after every launch (pft_comm_halo_deep)"""
+    meta, A = O.load_case("g20")
+    times = meta["traj_times"][:2]
+    res = _run_ranks(tmp_path, nranks, case="g20", times=times, tile=tile, pair=pair)
+    for r in res:
+        assert int(r["path"]) == 1 and int(r["pairs"]) == 1
+    for i in range(len(times)):
+        ref = meta["traj_m0"][i]
+        for r in res:
+            t, h, s, st, rc = r["rows"][i]
+            assert (t.hex(), h.hex(), int(s), int(st), int(rc)) == \
+                (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(), ref[2], ref[3], ref[4])
+        full = np.concatenate([r["states"][i] for r in res], axis=1)
+        assert np.array_equal(full, A[f"traj_m0_state{i}"])
+
+
 @pytest.mark.parametrize("nranks", [2, 4])
 def test_400_processes_equal_one_slab(tmp_path, nranks):
     steps = 12
@@ -89,8 +108,9 @@ def test_400_processes_equal_one_slab(tmp_path, nranks):
     x = sim.interior()
     sim.close()
     assert got[2] < got[3]                                    # a rejected step in the window
-    res = _run_ranks(tmp_path, nranks, case="default", grid_nodes=400, times=[1e9], steps=steps)
+    res = _run_ranks(tmp_path, nranks, case="default", grid_nodes=400, times=[1e9], steps=steps, pair=2)
     for r in res:
+        assert int(r["pairs"]) == 1                           # the pair kernels between the slabs
         t, h, s, st, rc = r["rows"][0]
         assert (t, h, int(s), int(st), int(rc)) == got + (2,)
     assert [int(r["n3"]) for r in res] == [400 // nranks] * nranks

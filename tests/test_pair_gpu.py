@@ -5,6 +5,7 @@ whose pair tiles fit exactly, leave partial tiles, are one tile wide or narrower
 forced z-chunks (interior chunks recompute stage A on the plane below and above), every calc_mode,
 gl_static, u_noise, and against the oracle and the reference's golden trajectory."""
 import ctypes as C
+import threading
 
 import numpy as np
 import pytest
@@ -29,7 +30,7 @@ def _run(dims, mode, pair, steps, kz=None, gl_static=False, noise=0.0, tile=2):
         Pm[O.PARAM_NAMES.index("u_noise_amp")] = noise
     n1, n2, n3 = dims
     L = P.lib()
-    L.pft_solver_set_option(P.PFT_OPT_PAIR, 1 if pair else 0)
+    L.pft_solver_set_option(P.PFT_OPT_PAIR, 2 if pair else 0)   # 2: also below the size threshold
     # u_noise comes from the C library's rand() (PrecalculateData, equation.c:450-456): the same
     # field for both runs
     C.CDLL("libc.so.6").srand(1)
@@ -112,7 +113,7 @@ def test_pair_golden_trajectory(mode, gl_static):
     ic = A["traj_m0_ic"] if mode not in (0, 1) else A[f"traj_m{mode}_ic"]
     runs = {}
     for pair in (1, 0):
-        P.lib().pft_solver_set_option(P.PFT_OPT_PAIR, pair)
+        P.lib().pft_solver_set_option(P.PFT_OPT_PAIR, 2 if pair else 0)
         sim = P.Simulation(info["n1"], info["n2"], info["n3"], (info["L1"], info["L2"], info["L3"]), mode, Pm,
                            initial=ic, tau=1.0, tau_min=info["tau_min"], delta=info["delta"], tile=2,
                            recompute=True, gl_static=gl_static)
@@ -141,3 +142,110 @@ def test_pair_full_size_400():
     ref, *_ = _run((200, 200, 400), 0, False, 20, tile=1)
     assert used == 1
     _same(got, ref)
+
+
+def _loopback_pairs(meta, initial, nprocs, times, dims=None, steps=0, gl_static=False, mode=0):
+    """nprocs slabs on one GPU (loopback transport, one host thread each), pair kernels forced"""
+    L = P.lib()
+    group = C.c_void_p()
+    assert L.pft_comm_init_loopback(C.byref(group), nprocs) == 0
+    out, errs = [None] * nprocs, []
+
+    def worker(r):
+        try:
+            mine = C.c_void_p()
+            assert L.pft_comm_loopback_rank(group, r, C.byref(mine)) == 0
+            L.pft_comm_set_current(mine)
+            L.pft_solver_set_option(P.PFT_OPT_PAIR, 2)         # per host thread
+            Pm, info = O.params_from_meta(meta)
+            n1, n2, n3 = dims or (info["n1"], info["n2"], info["n3"])
+            sim = P.Simulation(n1, n2, n3, (info["L1"], info["L2"], info["L3"]), mode, Pm, nprocs=nprocs, rank=r,
+                               initial=initial, beads=None if initial is not None else O.beads(), tau=1.0,
+                               tau_min=info["tau_min"], delta=info["delta"], gl_static=gl_static, tile=2)
+            res = []
+            for T in times:
+                rc = sim.solve_ex(T, steps, 0) if steps else sim.solve(T)
+                res.append((sim.t.hex(), sim.h.hex(), sim.system.steps, sim.system.steps_total, rc, sim.interior()))
+            out[r] = (res, sim.stats().pairs)
+            sim.close()
+            L.pft_solver_set_option(P.PFT_OPT_PAIR, 1)
+            L.pft_comm_set_current(None)
+            L.pft_comm_destroy(mine)
+        except BaseException as e:   # noqa: BLE001 -- surfaced below
+            errs.append(e)
+
+    ths = [threading.Thread(target=worker, args=(r,)) for r in range(nprocs)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=600)
+    L.pft_comm_destroy(group)
+    if errs:
+        raise errs[0]
+    return out
+
+
+@pytest.mark.parametrize("nprocs", [2, 3, 4])
+@pytest.mark.parametrize("gl_static", [False, True])
+def test_pair_multislab_loopback_golden(nprocs, gl_static):
+    """g20 (n3 = 20) on 2-4 slabs with the pair kernels: the reference's own trajectory bit for bit
+    (stage A on each ghost plane from the neighbour's two boundary planes)"""
+    meta, A = O.load_case("g20")
+    times = meta["traj_times"][:2]
+    out = _loopback_pairs(meta, A["traj_m0_ic"], nprocs, times, gl_static=gl_static)
+    assert all(o[1] == 1 for o in out)
+    for i in range(len(times)):
+        ref = meta["traj_m0"][i]
+        for o in out:
+            assert o[0][i][:5] == (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(), ref[2], ref[3], ref[4])
+        assert np.array_equal(np.concatenate([o[0][i][5] for o in out], axis=1), A[f"traj_m0_state{i}"])
+
+
+@pytest.mark.parametrize("nprocs,dims", [(3, (30, 30, 60)), (4, (66, 38, 21)), (2, (100, 36, 40))])
+def test_pair_multislab_loopback_equals_one_slab(nprocs, dims):
+    """default IC on grids with partial tiles and uneven slabs (21 planes over 4: 6/5/5/5), 10
+    attempted steps, against the single-slab pair run"""
+    ref, used, *_ = _run(dims, 0, True, 10)
+    meta, _ = O.load_case("g20")
+    out = _loopback_pairs(meta, None, nprocs, [1e9], dims=dims, steps=10)
+    assert used == 1 and all(o[1] == 1 for o in out)
+    for o in out:
+        assert o[0][0][:4] == ref[:4]
+    assert np.array_equal(np.concatenate([o[0][0][5] for o in out], axis=1), ref[4])
+
+
+@pytest.mark.parametrize("transport", ["rccl", "ipc"])
+def test_pair_self_exchange(transport):
+    """one slab, a 1-rank communicator exchanging with itself: the two-plane halo of every launch
+    runs through the transport (RCCL send/recv on the comm stream; ipc put kernel + flags) and
+    lands in planes a single slab never reads"""
+    import os
+    import uuid
+    meta, A = O.load_case("g20")
+    Pm, info = O.params_from_meta(meta)
+    if transport == "rccl":
+        L = P.lib()
+        uid = (C.c_char * 128)()
+        assert L.pft_comm_get_unique_id(uid) == 0
+        comm = C.c_void_p()
+        assert L.pft_comm_init_rccl(C.byref(comm), 1, 0, uid, 0) == 0
+        L.pft_comm_set_current(comm)
+    else:
+        comm = P.comm_init_ipc(1, 0, f"/pft_pselfx_{os.getpid()}_{uuid.uuid4().hex[:12]}")
+    try:
+        assert P.lib().pft_comm_set_self_exchange(comm, 1) == 0
+        P.lib().pft_solver_set_option(P.PFT_OPT_PAIR, 2)
+        sim = P.Simulation(info["n1"], info["n2"], info["n3"], (info["L1"], info["L2"], info["L3"]), 0, Pm,
+                           initial=A["traj_m0_ic"], tau=1.0, tau_min=info["tau_min"], delta=info["delta"], tile=2)
+        for i, T in enumerate(meta["traj_times"][:2]):
+            rc = sim.solve(T)
+            ref = meta["traj_m0"][i]
+            assert (sim.t.hex(), sim.h.hex(), sim.system.steps, sim.system.steps_total, rc) == \
+                (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(), ref[2], ref[3], ref[4])
+            assert np.array_equal(sim.interior(), A[f"traj_m0_state{i}"])
+        assert sim.stats().pairs == 1
+        sim.close()
+    finally:
+        P.lib().pft_solver_set_option(P.PFT_OPT_PAIR, 1)
+        P.lib().pft_comm_set_current(None)
+        P.comm_destroy(comm)
