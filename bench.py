@@ -238,13 +238,14 @@ def main():
         dom = max(per, key=lambda s: per[s][0])
         ms, byts = per[dom]
         achieved = byts / (ms * 1e-3) / 1e9
-        traffic, traffic_src = None, None
+        traffic, traffic_src, valu_frac = None, None, None
         pmc = os.path.join(REPO, "profiles", "pmc_summary.json")
         if os.path.exists(pmc) and not a.wave:
             try:
                 ps = json.load(open(pmc))
                 key = f"{'pair' if pairs else 'stage'}{dom}_gl{int(a.gl_static)}_{n1}x{n2}x{sim.grid.n3}_m{a.mode}"
                 traffic = ps.get(key, {}).get("hbm_bytes_per_launch")
+                valu_frac = ps.get(key, {}).get("valu_issue_frac")
                 if traffic is not None:
                     # not measured in this run: the calibrated FETCH_SIZE + WRITE_SIZE of that
                     # kernel from the rocprofv3 --pmc passes recorded in the file
@@ -254,6 +255,10 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": kernel_name(dom, a, rc_path, n1, pairs),
+                # the pair kernels are FP64-VALU-bound (stage A recomputed on a ring, no HBM bytes
+                # spared to compute): the fraction of the SIMDs' issue cycles their VALU
+                # instructions take, from the same PMC file (SQ_INSTS_VALU, GRBM_GUI_ACTIVE)
+                "valu_issue_frac": round(valu_frac, 4) if valu_frac is not None else None,
                 "algorithmic_bytes_per_launch": byts // nl[dom],
                 "avg_launch_ms": round(ms / nl[dom], 4),
                 "stages_ms": {str(s): round(per[s][0], 4) for s in per},

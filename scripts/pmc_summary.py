@@ -6,7 +6,11 @@ runs (FETCH_SIZE, WRITE_SIZE -- separate passes, MI355X_MICROARCH.md "rocprofv3 
 Corrections (MI355X_MICROARCH.md "HBM"): FETCH_SIZE/WRITE_SIZE are in KiB; gfx950's FETCH_SIZE
 is only exact for calibrated access widths, so the ratio known/measured of the probe_copy_kernel
 (8-byte loads and stores per lane, exactly the stage kernels' width, known byte count) calibrates
-both counters.  Output keys: stage<k>_gl<0|1>_<n1>x<n2>x<n3>_m<mode> (the slab's cells) -> HBM bytes per launch.
+both counters.  Output keys: stage<k>_gl<0|1>_<n1>x<n2>x<n3>_m<mode> (the slab's cells; pair<k> for
+the pair kernel whose second stage is k) -> HBM bytes per launch.  With a fourth run (SQ_INSTS_VALU
+and GRBM_GUI_ACTIVE in one pass), also the VALU issue fraction per kernel:
+  SQ_INSTS_VALU x 4 cycles (a wave64 VALU instruction on a 16-lane SIMD) / (1024 SIMDs x the
+  kernel's cycles, GRBM_GUI_ACTIVE / 8 XCDs) = SQ_INSTS_VALU / (32 GRBM_GUI_ACTIVE).
 """
 import csv
 import glob
@@ -38,13 +42,18 @@ def kname(k):
     m = re.search(r"merson_(?:stage|tile|fused)<(\d+),\s*(\d+),\s*(true|false)", k)
     if m:
         return f"stage{m.group(1)}", m.group(2), m.group(3) == "true"
+    m = re.search(r"merson_pair<(\d+),\s*(\d+),\s*(true|false)", k)
+    if m:
+        return f"pair{int(m.group(1)) + 1}", m.group(2), m.group(3) == "true"
     if "probe_copy" in k:
         return "probe", None, None
     return None, None, None
 
 
-def main(trace_dir, fetch_dir, write_dir, dims, probe_bytes, out_path):
+def main(trace_dir, fetch_dir, write_dir, dims, probe_bytes, out_path, valu_dir=None):
     fetch, write = counters(fetch_dir, "FETCH_SIZE"), counters(write_dir, "WRITE_SIZE")
+    valu = counters(valu_dir, "SQ_INSTS_VALU") if valu_dir else {}
+    grbm = counters(valu_dir, "GRBM_GUI_ACTIVE") if valu_dir else {}
     pf = [v for k, v in fetch.items() if kname(k)[0] == "probe"]
     pw = [v for k, v in write.items() if kname(k)[0] == "probe"]
     cal_f = probe_bytes / (pf[0] * 1024) if pf else 1.0
@@ -65,10 +74,15 @@ def main(trace_dir, fetch_dir, write_dir, dims, probe_bytes, out_path):
         key = f"{st}_gl{int(gls)}_{dims}_m{mode}"
         res[key] = {"kernel": k, "fetch_bytes": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
                     "raw_FETCH_SIZE_KiB": fetch.get(k), "raw_WRITE_SIZE_KiB": write.get(k)}
+        if k in valu and grbm.get(k):
+            res[key]["SQ_INSTS_VALU"] = valu[k]
+            res[key]["GRBM_GUI_ACTIVE"] = grbm[k]
+            res[key]["valu_issue_frac"] = valu[k] / (32.0 * grbm[k])
     res["kernel_stats"] = stats
     # where these numbers come from (bench.py copies this into roofline.traffic_source)
-    res["provenance"] = {"tool": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes of "
-                                 "bench.py (scripts/evidence.sh); FETCH_SIZE x fetch_factor from the probe copy",
+    res["provenance"] = {"tool": "rocprofv3 --pmc FETCH_SIZE, --pmc WRITE_SIZE and --pmc SQ_INSTS_VALU "
+                                 "GRBM_GUI_ACTIVE, separate passes of bench.py (scripts/evidence.sh); "
+                                 "FETCH_SIZE x fetch_factor from the probe copy",
                          "tag": os.environ.get("TAG", ""),
                          "date": os.environ.get("PMC_DATE", ""),
                          "git": os.environ.get("PMC_GIT", "")}
@@ -78,4 +92,5 @@ def main(trace_dir, fetch_dir, write_dir, dims, probe_bytes, out_path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), sys.argv[6])
+    main(sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), sys.argv[6],
+         sys.argv[7] if len(sys.argv) > 7 else None)
