@@ -1475,6 +1475,8 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
     }
 
     PFT_PAIR_BIND(A2, C2);
+    // (a build that skips this re-load -- wrong results, timing only -- ran 1% faster: the
+    // re-load's latency hides behind stage B's stencil)
     if (LATE && SA == 4 && kB >= kb && isB) pair_load<SA>(A2, pbo(mm - 1), ro);
     if (LATE_LA && mm + 2 <= mlast) pair_load<SA>(A2, pbo(mm + 2), rnn);
     if (kB >= kb && isB) {
