@@ -29,7 +29,9 @@ def need_gpu():
         pytest.fail("no HIP device: the gpu tests must run on an MI355X (no CPU fallback exists)")
 
 
-def _run(name, flavour_tile=None):
+def _run(name, flavour_tile=None, pair=1):
+    """pair 2: stages 2+3 and 4+5 as pair kernels (PFT_OPT_PAIR; needs an LDS-tiled flavour)"""
+    P.lib().pft_solver_set_option(P.PFT_OPT_PAIR, pair)
     meta, A = O.load_case("ctl")
     run = meta["runs"][name]
     Pm, info = O.params_from_meta(meta)
@@ -59,7 +61,10 @@ def _run(name, flavour_tile=None):
     finally:
         L.RK_MPI_SA_handle_NAN(0)
         path = sim.stats().path
+        pairs = sim.stats().pairs
         sim.close()
+        L.pft_solver_set_option(P.PFT_OPT_PAIR, 1)
+    assert pairs == (pair == 2)
     return run, A, rows, log, states, path
 
 
@@ -67,29 +72,30 @@ def _ref_rows(run):
     return [[float.fromhex(r[0]).hex(), float.fromhex(r[1]).hex()] + r[2:] for r in run["traj"]]
 
 
+@pytest.mark.parametrize("tile,pair", [(None, 1), (2, 2)])
 @pytest.mark.parametrize("name", ["nan_giveup_a", "nan_giveup_b", "nan_giveup_c"])
-def test_nan_gives_up_like_the_reference(name):
-    run, A, rows, log, states, path = _run(name)
+def test_nan_gives_up_like_the_reference(name, tile, pair):
+    run, A, rows, log, states, path = _run(name, tile, pair)
     assert path == 1
     assert rows == _ref_rows(run)
     assert rows[0][4] == -4 and rows[0][5] == 1
     assert np.array_equal(states[0], A[f"{name}_state0"], equal_nan=True)
 
 
-@pytest.mark.parametrize("tile", [None, 32])
-def test_nan_retries_then_recovers_like_the_reference(tile):
+@pytest.mark.parametrize("tile,pair", [(None, 1), (32, 1), (32, 2)])
+def test_nan_retries_then_recovers_like_the_reference(tile, pair):
     """tile None: the automatic choice (the cache kernel, aux arrays, for this 10-cell plane); 32: the
-    fused LDS-tiled recompute kernel with the speculative stage 1"""
-    run, A, rows, log, states, path = _run("nan_retry", tile)
+    fused LDS-tiled recompute kernel with the speculative stage 1; pair 2: and the pair kernels"""
+    run, A, rows, log, states, path = _run("nan_retry", tile, pair)
     assert rows == _ref_rows(run)
     assert rows[0][3] - rows[0][2] > 1 and rows[0][5] == 1      # retries happened, NaN seen
     assert log == [[c[0], float.fromhex(c[1]).hex(), float.fromhex(c[2]).hex()] for c in run["cb"]]
     assert np.array_equal(states[0], A["nan_retry_state0"])
 
 
-@pytest.mark.parametrize("tile", [None, 32])
-def test_service_callback_break_and_resume_like_the_reference(tile):
-    run, A, rows, log, states, path = _run("cb_break", tile)
+@pytest.mark.parametrize("tile,pair", [(None, 1), (32, 1), (32, 2)])
+def test_service_callback_break_and_resume_like_the_reference(tile, pair):
+    run, A, rows, log, states, path = _run("cb_break", tile, pair)
     assert rows == _ref_rows(run)
     assert rows[0][4] == 1 and rows[1][4] == 0
     assert log == [[c[0], float.fromhex(c[1]).hex(), float.fromhex(c[2]).hex()] for c in run["cb"]]
