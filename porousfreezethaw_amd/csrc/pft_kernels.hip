@@ -1804,6 +1804,8 @@ struct pft_slab {
   int pair_on;           // pair kernels (merson_pair): 0 off, 1 automatic (large slabs), 2 wherever
                          // they fit (pft_slab_set_pair); env PFT_PAIR overrides
   int pair_env;          // PFT_PAIR was set
+  int pair_tx, pair_ty;  // pair tile (pair_geometry, once per slab); 0 x 0: none fits
+  long pair_ntile;
   // per-stage timing: a ring of begin/end event pairs, so that kernels still running when the
   // host collects (the speculative stage 1) are picked up by a later collect
   hipEvent_t tev[6][PFT_TRING][2];
@@ -1837,6 +1839,8 @@ int pft_hip_device_sync(void)
   return 0;
 }
 
+static long pair_geometry(int n1, int n2, int* tx_out, int* ty_out);
+
 int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
 {
   *out = nullptr;
@@ -1868,6 +1872,7 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
     const char* ep = getenv("PFT_PAIR");
     s->pair_env = ep != nullptr;
     s->pair_on = ep ? atoi(ep) : 1;
+    s->pair_ntile = pair_geometry(d->n1, d->n2, &s->pair_tx, &s->pair_ty);
   }
   const size_t bytes = sizeof(double) * (3 * (size_t)s->fs + 2 * (size_t)s->plane);
   hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
@@ -2685,7 +2690,9 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
   if (k_end <= k_begin) return 0;
   a.k_begin = k_begin;
   a.k_end = k_end;
-  if (pair_geometry(a.n1, a.n2, &a.tx, &a.ty) <= 0 || !pair_geometry_ok(a.tx, a.ty)) return -2;
+  a.tx = s->pair_tx;
+  a.ty = s->pair_ty;
+  if (s->pair_ntile <= 0 || !pair_geometry_ok(a.tx, a.ty)) return -2;
   a.ntx = (a.n1 + a.tx - 1) / a.tx;
   a.ntile = a.ntx * ((a.n2 + a.ty - 1) / a.ty);
   const int nplanes = k_end - k_begin;
@@ -2762,25 +2769,25 @@ int pft_slab_set_pair(pft_slab* s, int on)
 
 int pft_slab_pair_ok(const pft_slab* s)
 {
-  int tx, ty;
-  // 32-bit byte offsets within a field (merson_pair's loads and stores)
   // automatic: slabs of at least PFT_PAIR_MIN_CELLS_PER_CU cells per CU.  Measured (A/B, one box):
-  // 400^3 +14%, the 800^3 8-way rank slab +12%, the 64 M-cell cube +18%, but 200^3 (2 M cells)
-  // -3.5% and 100^3 -4.5%, where the chunks' extra stage-A planes and the launch latency of
-  // fewer, longer workgroups dominate
+  // 400^3 +8..14%, the 800^3 8-way rank slab +8..12%, the 64 M-cell cube +18%, but 200^3 (2 M
+  // cells) -3.5% and 100^3 -4.5%, where the chunks' extra stage-A planes and the launch latency
+  // of fewer, longer workgroups dominate
   if (s->pair_on == 1 && (double)s->plane * s->d.n3 < (double)s->n_cu * PFT_PAIR_MIN_CELLS_PER_CU) return 0;
   // z-neighbours: the two-plane halo (pft_comm_halo_deep) needs n3 >= 2, and stage A on a ghost
   // plane would need the neighbour's u_noise there (not exchanged: one launch per stage then)
   const bool nb = s->d.has_below || s->d.has_above;
   if (nb && (s->d.n3 < 2 || s->noise)) return 0;
+  // (merson_pair addresses a field with 32-bit byte offsets)
   return PFT_GLK_LITERAL && s->pair_on && slab_kind(s) == KFUSED &&
-         (double)s->fs * 8.0 < 4294967296.0 && pair_geometry(s->d.n1, s->d.n2, &tx, &ty) > 0;
+         (double)s->fs * 8.0 < 4294967296.0 && s->pair_ntile > 0;
 }
 
 int pft_slab_pair_geometry(const pft_slab* s, int* tx, int* ty)
 {
-  *tx = *ty = 0;
-  return pair_geometry(s->d.n1, s->d.n2, tx, ty) > 0 ? 0 : -2;
+  *tx = s->pair_tx;
+  *ty = s->pair_ty;
+  return s->pair_ntile > 0 ? 0 : -2;
 }
 
 int pft_slab_pair(pft_slab* s, int first, double t_a, double t_b, double h, double coef)
