@@ -58,7 +58,7 @@ def _same(a, b):
 # pair tiles (pair_geometry): 30 -> 30 cells wide (one tile), 100x36 -> 34 x 16 ish, 18x12 one
 # tile, 66x38 partial x tile, 252x14 / 318x10 wide planes, 2 x 6 and 4 x 130 narrow ones
 GRIDS = [(30, 30, 60), (100, 36, 40), (18, 12, 30), (66, 38, 21), (252, 14, 6), (318, 10, 5), (2, 6, 5),
-         (4, 130, 9), (50, 50, 100)]
+         (4, 130, 9), (50, 50, 100), (30, 30, 2)]
 
 
 @pytest.mark.parametrize("dims", GRIDS)
@@ -201,10 +201,12 @@ def test_pair_multislab_loopback_golden(nprocs, gl_static):
         assert np.array_equal(np.concatenate([o[0][i][5] for o in out], axis=1), A[f"traj_m0_state{i}"])
 
 
-@pytest.mark.parametrize("nprocs,dims", [(3, (30, 30, 60)), (4, (66, 38, 21)), (2, (100, 36, 40))])
+@pytest.mark.parametrize("nprocs,dims", [(3, (30, 30, 60)), (4, (66, 38, 21)), (2, (100, 36, 40)),
+                                          (4, (30, 30, 12)), (3, (18, 12, 8))])
 def test_pair_multislab_loopback_equals_one_slab(nprocs, dims):
-    """default IC on grids with partial tiles and uneven slabs (21 planes over 4: 6/5/5/5), 10
-    attempted steps, against the single-slab pair run"""
+    """default IC on grids with partial tiles and uneven slabs (21 planes over 4: 6/5/5/5; slabs of
+    2-3 planes, where the whole slab is launched before its two-plane exchange), 10 attempted
+    steps, against the single-slab pair run"""
     ref, used, *_ = _run(dims, 0, True, 10)
     meta, _ = O.load_case("g20")
     out = _loopback_pairs(meta, None, nprocs, [1e9], dims=dims, steps=10)
