@@ -1154,6 +1154,13 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT
 #ifndef PFT_PAIR_SCHED
 #define PFT_PAIR_SCHED 0
 #endif
+// wave priorities in the pair kernels' z-loop (merson_pair, PRIO): pair 2+3, pair 4+5
+#ifndef PFT_PAIR_PRIO2
+#define PFT_PAIR_PRIO2 1
+#endif
+#ifndef PFT_PAIR_PRIO4
+#define PFT_PAIR_PRIO4 2
+#endif
 #ifndef PFT_PAIR_LATE_LA_MASK
 #define PFT_PAIR_LATE_LA_MASK 0
 #endif
@@ -1403,6 +1410,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   // LATE_LA: the look-ahead load after stage A as well (else at the top: it then has a whole
   // iteration to land, and waiting for the output re-load at the end of stage B drains it)
   constexpr bool LATE_LA = ((PFT_PAIR_LATE_LA_MASK >> SA) & 1) != 0;
+  constexpr int PRIO = SA == 2 ? PFT_PAIR_PRIO2 : PFT_PAIR_PRIO4;
   PairRaw rn, rnn, rcr;
   dbl2 kao[2] = {zero2, zero2};  // stage A's K (u, p) at plane mm - 1
   FaceT fzA[2], fzB[2];
@@ -1453,6 +1461,15 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
     if (!LATE_LA && mm + 2 <= mlast) pair_load<SA>(A0, pbo(mm + 2), rnn);          // look-ahead
 
     PFT_PAIR_BIND(A1, C1);
+    // The two waves of a SIMD (w and w + 4) run the same phase between two barriers, so their
+    // stalls coincide.  PRIO: waves 0-3 get issue precedence in stage A (1: waves 4-7 in stage B,
+    // 2: nobody in stage B), so the two drift apart and fill each other's stalls.  Measured (A/B,
+    // one box): pair 4+5 0.496 -> 0.483 ms (1) / 0.480 ms (2); pair 2+3 0.407 -> 0.406 (1) /
+    // 0.415 (2); precedence by wave parity instead of halves: slower (0.505).
+    if (PRIO) {
+      if ((threadIdx.x >> 8) == 0) __builtin_amdgcn_s_setprio(2);
+      else __builtin_amdgcn_s_setprio(0);
+    }
     dbl2 ka[2] = {zero2, zero2};
     if (mm <= mA1 && isA) {
       // stage A at plane mm, evaluated as the acting pair's thread does
@@ -1475,6 +1492,12 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
     }
 
     PFT_PAIR_BIND(A2, C2);
+    if (PRIO == 2) {
+      __builtin_amdgcn_s_setprio(0);
+    } else if (PRIO == 1) {
+      if ((threadIdx.x >> 8) == 0) __builtin_amdgcn_s_setprio(0);
+      else __builtin_amdgcn_s_setprio(2);
+    }
     // (a build that skips this re-load -- wrong results, timing only -- ran 1% faster: the
     // re-load's latency hides behind stage B's stencil)
     if (LATE && SA == 4 && kB >= kb && isB) pair_load<SA>(A2, pbo(mm - 1), ro);
