@@ -1200,10 +1200,10 @@ static constexpr unsigned PFT_PAIR_COFF =
 // empty asm, so the loads cannot be hoisted out of the loop).  Kept live across the whole loop,
 // the ~25 model constants, the array bases and the step coefficients needed ~190 SGPRs: ~90 were
 // spilled into VGPR lanes and re-read by ~160 v_readlane per iteration.
-// Pairs (bit SA) that do so: pair 4+5 (0.519 -> 0.486 ms at 400^3); pair 2+3, which spilled ~15
-// SGPRs, measured 2% slower with it.
+// Pairs (bit SA) that do so: both -- pair 4+5 0.519 -> 0.486 ms at 400^3; pair 2+3 (~15 SGPRs
+// spilled) 0.408 -> 0.403 ms once the wave priorities below were in (2% slower before them).
 #ifndef PFT_PAIR_KREL_MASK
-#define PFT_PAIR_KREL_MASK (1 << 4)
+#define PFT_PAIR_KREL_MASK ((1 << 2) | (1 << 4))
 #endif
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef const __attribute__((address_space(4))) char* pft_kptr;
