@@ -40,6 +40,7 @@ import porousfreezethaw_amd as P  # noqa: E402
 from porousfreezethaw_amd import params as PR  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6        # FP64 vector: half the guide's 157.3 TF FP32 vector peak (16 FP64 lanes per SIMD and cycle)
 # algorithmic HBM bytes per cell of each fused stage kernel: doubles read
 # once + written once, perfect stencil reuse.  faithful: u, p, gl all evolved by the solver;
 # gl_static: dgl == 0 exploited (PFT_OPT_GL_STATIC)
@@ -238,7 +239,7 @@ def main():
         dom = max(per, key=lambda s: per[s][0])
         ms, byts = per[dom]
         achieved = byts / (ms * 1e-3) / 1e9
-        traffic, traffic_src, valu_frac = None, None, None
+        traffic, traffic_src, valu_frac, f64 = None, None, None, {}
         pmc = os.path.join(REPO, "profiles", "pmc_summary.json")
         if os.path.exists(pmc) and not a.wave:
             try:
@@ -246,6 +247,7 @@ def main():
                 key = f"{'pair' if pairs else 'stage'}{dom}_gl{int(a.gl_static)}_{n1}x{n2}x{sim.grid.n3}_m{a.mode}"
                 traffic = ps.get(key, {}).get("hbm_bytes_per_launch")
                 valu_frac = ps.get(key, {}).get("valu_issue_frac")
+                f64 = {q: ps.get(key, {}).get(q) for q in ("fp64_flop_per_launch", "fp64_pipe_busy_frac")}
                 if traffic is not None:
                     # not measured in this run: the calibrated FETCH_SIZE + WRITE_SIZE of that
                     # kernel from the rocprofv3 --pmc passes recorded in the file
@@ -259,6 +261,14 @@ def main():
                 # spared to compute): the fraction of the SIMDs' issue cycles their VALU
                 # instructions take, from the same PMC file (SQ_INSTS_VALU, GRBM_GUI_ACTIVE)
                 "valu_issue_frac": round(valu_frac, 4) if valu_frac is not None else None,
+                # the same kernel against the FP64 vector roof: its FP64 FLOP per launch (PMC, same
+                # file: 64 lanes x (ADD + MUL + TRANS + 2 FMA) wave instructions) / this run's
+                # launch time, and the FP64 pipe's busy fraction (4 cycles per wave64 instruction)
+                "fp64": ({"achieved": round(f64["fp64_flop_per_launch"] / (ms / nl[dom] * 1e-3) / 1e12, 2),
+                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                          "frac": round(f64["fp64_flop_per_launch"] / (ms / nl[dom] * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 4),
+                          "pipe_busy_frac": round(f64["fp64_pipe_busy_frac"], 4)}
+                         if f64.get("fp64_flop_per_launch") else None),
                 "algorithmic_bytes_per_launch": byts // nl[dom],
                 "avg_launch_ms": round(ms / nl[dom], 4),
                 "stages_ms": {str(s): round(per[s][0], 4) for s in per},

@@ -1,7 +1,10 @@
 #!/bin/bash
+# FP64 issue of the pair and stage kernels (the compute roof of the pair kernels): the FP64 VALU
+# instruction classes, the VALU-active quad-cycles and the kernel's cycles, one --pmc pass each
+# line (never combined with other tracing).  -> gpurun_out/pmc_fp64/table.txt
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-OUT=gpurun_out/${PMC_OUT:-pmc_pair}
+OUT=gpurun_out/pmc_fp64
 mkdir -p $OUT
 ARGS="--steps 10 --warmup 2 --no-cpu --timing-steps 0"
 i=0
@@ -12,9 +15,8 @@ while read -r counters; do
   rc=$?; echo "pass $i ($counters) rc=$rc"
   [ $rc -ne 0 ] && exit $rc
 done <<'LIST'
-SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU
-SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR
-GRBM_GUI_ACTIVE GRBM_COUNT
+SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE
+SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_SALU SQ_BUSY_CYCLES
 LIST
 python3 - "$OUT" <<'PY'
 import csv, glob, sys, collections, os
@@ -26,6 +28,6 @@ for f in glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), rec
 with open(os.path.join(out, "table.txt"), "w") as fh:
     for k, v in sorted(acc.items()):
         if "merson" not in k: continue
-        line = k[:40] + " | " + " ".join(f"{c}={sum(x)/len(x):.4g}" for c, x in sorted(v.items()))
+        line = k[:40] + " | " + " ".join(f"{c}={sum(x)/len(x):.6g}" for c, x in sorted(v.items()))
         print(line); fh.write(line + "\n")
 PY

@@ -11,6 +11,10 @@ the pair kernel whose second stage is k) -> HBM bytes per launch.  With a fourth
 and GRBM_GUI_ACTIVE in one pass), also the VALU issue fraction per kernel:
   SQ_INSTS_VALU x 4 cycles (a wave64 VALU instruction on a 16-lane SIMD) / (1024 SIMDs x the
   kernel's cycles, GRBM_GUI_ACTIVE / 8 XCDs) = SQ_INSTS_VALU / (32 GRBM_GUI_ACTIVE).
+With a fifth run (SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 and GRBM_GUI_ACTIVE in one pass,
+scripts/pmc_fp64.sh), the FP64 work per launch: FLOP = 64 lanes x (ADD + MUL + TRANS + 2 FMA)
+wave instructions, and the FP64 pipe's busy fraction = 4 cycles per wave64 FP64 instruction (16
+FP64 lanes per SIMD and cycle: the 78.6 TFLOP/s vector peak) / (1024 SIMDs x the kernel's cycles).
 """
 import csv
 import glob
@@ -50,8 +54,10 @@ def kname(k):
     return None, None, None
 
 
-def main(trace_dir, fetch_dir, write_dir, dims, probe_bytes, out_path, valu_dir=None):
+def main(trace_dir, fetch_dir, write_dir, dims, probe_bytes, out_path, valu_dir=None, fp64_dir=None):
     fetch, write = counters(fetch_dir, "FETCH_SIZE"), counters(write_dir, "WRITE_SIZE")
+    f64 = {c: counters(fp64_dir, "SQ_INSTS_VALU_" + c + "_F64") for c in ("ADD", "MUL", "FMA", "TRANS")} if fp64_dir else {}
+    grbm64 = counters(fp64_dir, "GRBM_GUI_ACTIVE") if fp64_dir else {}
     valu = counters(valu_dir, "SQ_INSTS_VALU") if valu_dir else {}
     grbm = counters(valu_dir, "GRBM_GUI_ACTIVE") if valu_dir else {}
     pf = [v for k, v in fetch.items() if kname(k)[0] == "probe"]
@@ -78,10 +84,17 @@ def main(trace_dir, fetch_dir, write_dir, dims, probe_bytes, out_path, valu_dir=
             res[key]["SQ_INSTS_VALU"] = valu[k]
             res[key]["GRBM_GUI_ACTIVE"] = grbm[k]
             res[key]["valu_issue_frac"] = valu[k] / (32.0 * grbm[k])
+        if f64 and all(k in f64[c] for c in f64) and grbm64.get(k):
+            ins = {c: f64[c][k] for c in f64}
+            n = ins["ADD"] + ins["MUL"] + ins["FMA"] + ins["TRANS"]
+            res[key]["fp64_wave_insts"] = ins
+            res[key]["fp64_flop_per_launch"] = 64.0 * (n + ins["FMA"])
+            res[key]["fp64_pipe_busy_frac"] = 4.0 * n / (1024.0 * grbm64[k] / 8.0)
     res["kernel_stats"] = stats
     # where these numbers come from (bench.py copies this into roofline.traffic_source)
     res["provenance"] = {"tool": "rocprofv3 --pmc FETCH_SIZE, --pmc WRITE_SIZE and --pmc SQ_INSTS_VALU "
-                                 "GRBM_GUI_ACTIVE, separate passes of bench.py (scripts/evidence.sh); "
+                                 "GRBM_GUI_ACTIVE, --pmc SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 GRBM_GUI_ACTIVE, "
+                                 "separate passes of bench.py (scripts/evidence.sh); "
                                  "FETCH_SIZE x fetch_factor from the probe copy",
                          "tag": os.environ.get("TAG", ""),
                          "date": os.environ.get("PMC_DATE", ""),
@@ -93,4 +106,4 @@ def main(trace_dir, fetch_dir, write_dir, dims, probe_bytes, out_path, valu_dir=
 
 if __name__ == "__main__":
     main(sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]), sys.argv[6],
-         sys.argv[7] if len(sys.argv) > 7 else None)
+         sys.argv[7] if len(sys.argv) > 7 else None, sys.argv[8] if len(sys.argv) > 8 else None)
