@@ -25,6 +25,7 @@ kernel, HIP-event timed) and `cpu_baseline` (the CPU oracle port on a bounded sa
 """
 import argparse
 import ctypes as C
+import hashlib
 import json
 import os
 import sys
@@ -111,6 +112,9 @@ def parse():
     ap.add_argument("--wave", type=int, default=0,
                     help="W > 0: a step's five stages as a skewed z-wavefront of W-plane launches "
                          "(PFT_OPT_WAVE; N = 1)")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="N > 1: skip the decomposition-invariance check (rank 0 re-runs the same attempted "
+                         "steps on one slab of its own GPU and compares every rank's state bit for bit)")
     ap.add_argument("--probe", type=int, default=0,
                     help="after the run, launch the 8-B/lane copy probe this many times "
                          "(rocprofv3 FETCH_SIZE/WRITE_SIZE calibration, known bytes)")
@@ -185,7 +189,8 @@ def main():
         sim.system.Service_Callback = C.cast(service, C.c_void_p).value
 
     # warm-up: uploads x once, builds the kernels' caches; W attempted steps
-    rc = sim.solve_ex(final_time, max(1, a.warmup), P.PFT_SOLVE_KEEP_DEVICE)
+    calls = [max(1, a.warmup)]                 # the capped solve calls, in order (the parity re-run repeats them)
+    rc = sim.solve_ex(final_time, calls[0], P.PFT_SOLVE_KEEP_DEVICE)
     assert rc == 2, rc
     st0 = sim.system.steps_total
     barrier()
@@ -195,6 +200,7 @@ def main():
     barrier()
     t2 = time.perf_counter()
     assert rc == 2, rc
+    calls.append(a.steps)
     steps = sim.system.steps_total - st0
     assert steps == a.steps, (steps, a.steps)
     el = t2 - t1
@@ -211,6 +217,7 @@ def main():
         L.pft_solver_set_option(P.PFT_OPT_TIMING, 2)
         rc = sim.solve_ex(final_time, a.timing_steps, P.PFT_SOLVE_KEEP_DEVICE | P.PFT_SOLVE_REUSE_DEVICE)
         assert rc == 2, rc
+        calls.append(a.timing_steps)
         L.pft_solver_set_option(P.PFT_OPT_TIMING, 0)
     stats = sim.stats()
     geo = sim.tile_geometry()
@@ -336,15 +343,76 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu:
         cpu = cpu_baseline(sim, base, a)
     out["cpu_baseline"] = cpu
+    mine = slab_digest(sim) if (world > 1 and not a.no_parity) else None
     sim.close()
     if comm is not None:
         L.pft_comm_set_current(None)
         L.pft_comm_destroy(comm)
+
+    # ---- N > 1: decomposition invariance, checked on every run --------------------
+    ok = True
+    if mine is not None:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+        if rank == 0:
+            out["parity"] = parity_check(ranks, calls, a, base, (n1, n2, total_n3), Ls, beads, final_time, dev)
+            ok = out["parity"]["equal"]
+        dist.barrier()                        # the other ranks wait for rank 0's single-slab re-run
+    else:
+        out["parity"] = None
     if rank == 0:
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist is not None:
         dist.destroy_process_group()
+    if not ok:
+        sys.exit(f"parity: the {world}-slab run differs from the single-slab run of the same steps")
+
+
+def slab_digest(sim):
+    """this rank's trajectory position and the SHA-256 of its interior (u, p, gl planes of the slab)"""
+    sim.download()
+    g = sim.grid
+    return {"t": float(sim.t).hex(), "h": float(sim.h).hex(), "steps": int(sim.system.steps),
+            "steps_total": int(sim.system.steps_total), "first_row": int(g.first_row), "n3": int(g.n3),
+            "sha256": hashlib.sha256(sim.interior().tobytes()).hexdigest()}
+
+
+def parity_check(ranks, calls, a, base, dims, Ls, beads, final_time, dev):
+    """Rank 0 re-runs the N-slab benchmark's exact solve calls (the same attempted-step caps, from the
+    same initial condition) on ONE slab on its own GPU, and compares every rank's (t, h, steps,
+    steps_total) and the SHA-256 of its planes with the single slab's.  The reference's results do
+    not depend on the decomposition (bitwise across rank counts), so any difference --
+    a wrong halo pairing, a stale ghost plane -- fails the run."""
+    L = P.lib()
+    t0 = time.time()
+    n1, n2, total_n3 = dims
+    L.pft_comm_set_current(None)
+    L.pft_hip_set_device(dev)
+    ref = P.Simulation(n1, n2, total_n3, Ls, a.mode, P.params_array(base), nprocs=1, rank=0, beads=beads,
+                       tau=base["tau"], tau_min=base["tau_min"], delta=base["delta"], gl_static=a.gl_static,
+                       kz=a.kz or None, tile=a.tile, recompute=not a.no_recompute)
+    for i, k in enumerate(calls):
+        flags = P.PFT_SOLVE_KEEP_DEVICE | (P.PFT_SOLVE_REUSE_DEVICE if i else 0)
+        rc = ref.solve_ex(final_time, k, flags)
+        assert rc == 2, rc
+    ref.download()
+    x = ref.interior()
+    pairs = bool(ref.stats().pairs)
+    bad = []
+    for r, m in enumerate(ranks):
+        f, n = m["first_row"], m["n3"]
+        want = {"t": float(ref.t).hex(), "h": float(ref.h).hex(), "steps": int(ref.system.steps),
+                "steps_total": int(ref.system.steps_total),
+                "sha256": hashlib.sha256(np.ascontiguousarray(x[:, f:f + n]).tobytes()).hexdigest()}
+        diff = [k for k in want if want[k] != m[k]]
+        if diff:
+            bad.append({"rank": r, "fields": diff})
+    ref.close()
+    return {"equal": not bad, "attempted_steps": int(sum(calls)), "calls": calls, "ranks": len(ranks),
+            "reference": "one slab on rank 0's GPU, same initial condition and solve calls"
+                         + (" (pair kernels)" if pairs else ""),
+            "mismatches": bad, "seconds": round(time.time() - t0, 1)}
 
 
 def make_comm(L, transport, world, rank, dev, dist):

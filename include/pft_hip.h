@@ -233,6 +233,14 @@ int pft_slab_halo_signal(pft_slab * s, unsigned long long seq);
    neighbours' ghost planes (the fused kernel does, with neighbours set); clears the mark */
 int pft_slab_take_pushed(pft_slab * s, int role);
 int pft_slab_halo_wait(pft_slab * s, unsigned long long seq);
+/* The host waits for the compute stream.  With ipc neighbours attached every host wait of the
+   slab (this one, up/download, the error-norm fetch) is bounded by PFT_IPC_TIMEOUT seconds
+   (default 300): a peer that died or diverged never raises the flag the stream waits on, so on
+   expiry the slab releases its own flags, drains the stream and returns PFT_ERR_IPC_TIMEOUT
+   (RK_MPI_SA_solve: PFT_SOLVE_DEVICE_ERROR).  set_peer refuses (-2) a neighbour on another GPU
+   unless PFT_IPC_CROSS_GPU=1: cross-GPU ipc halos are not verified on hardware. */
+#define PFT_ERR_IPC_TIMEOUT (-5002)
+int pft_slab_sync(pft_slab * s);
 
 /* peer copy of one ghost plane between slabs on the same process (loopback transport) */
 int pft_memcpy_d2d_async(void * dst, const void * src, size_t bytes, void * stream);

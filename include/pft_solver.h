@@ -69,7 +69,10 @@ enum {
 	                           inside stage B's stencil, never stored -- 21 instead of 39 doubles
 	                           per cell-step, bit-identical): 1 (default) = on slabs of at least
 	                           16 Ki cells per CU (4 M cells on MI355X), 2 = on any slab they fit,
-	                           0 = one launch per stage */
+	                           0 = one launch per stage */,
+	PFT_OPT_FAIL_RHS = 11   /* test hook: N > 0 makes the N-th device evaluation of libpft's own
+	                           right-hand side on a host array (f_generic_model01/2 called by the
+	                           host-staged path) fail as a device fault would; 0 (default) off */
 };
 int pft_solver_set_option(int opt, long value);
 

@@ -32,6 +32,7 @@ PFT_OPT_ONE_STREAM = 7
 PFT_OPT_WAVE = 8
 PFT_OPT_LAZY_ALLOC = 9
 PFT_OPT_PAIR = 10
+PFT_OPT_FAIL_RHS = 11
 PFT_SOLVE_DEVICE_ERROR = -7
 MPI_COMM_WORLD = 0x44000000
 
@@ -56,6 +57,7 @@ class RK_MPI_S_SOLUTION(C.Structure):
 
 
 SERVICE_FN = C.CFUNCTYPE(C.c_int, C.c_double, C.POINTER(RK_MPI_S_SOLUTION))
+REARRANGE_FN = C.CFUNCTYPE(C.POINTER(RK_MEM_DIST), C.POINTER(RK_MEM_DIST))
 RK_MPI_S_SOLUTION._fields_ = [
     ("n", C.POINTER(RK_MEM_DIST)), ("t", C.c_double), ("x", C.POINTER(C.c_double)),
     ("meta_f", C.c_void_p), ("h", C.c_double), ("h_min", C.c_double), ("delta", C.c_double),

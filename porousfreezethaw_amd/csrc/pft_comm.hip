@@ -355,8 +355,13 @@ static int ipc_attach(pft_comm* c, pft_slab* s)
   IpcRound* recs;
   int rc;
   if (c->slab) {
-    // nobody may still write into the buffers about to be unmapped (or freed)
-    HCHK(hipStreamSynchronize((hipStream_t)pft_slab_stream(c->slab)));
+    // nobody may still write into the buffers about to be unmapped (or freed); bounded by the
+    // slab's ipc timeout (a lost peer's flag never comes)
+    if ((rc = pft_slab_sync(c->slab))) {
+      pft_slab_ipc_close(c->slab);
+      c->slab = nullptr;
+      return rc;
+    }
     if ((rc = ipc_round(c, nullptr, 0, nullptr, 0, &recs))) return rc;
     pft_slab_ipc_close(c->slab);
     c->slab = nullptr;

@@ -1791,6 +1791,7 @@ struct pft_slab {
                                  // above (monotonic exchange sequence numbers); [8] put counter
   SlabPeer peer[2];              // [0] the neighbour below, [1] above
   int fused_push;                // ipc: the fused kernels push (PFT_IPC_FUSED_PUSH, default 0)
+  int drop_puts;                 // fault injection: halo puts and flag raises skipped (PFT_IPC_DROP_PUTS)
   int pushed_role;               // buffer role whose boundary planes the last stage launch pushed
                                  // into the neighbours (merson_fused), -1: none
   double* staging;       // host padded layout on the device (for upload/download)
@@ -1829,6 +1830,8 @@ struct pft_slab {
   int pair_env;          // PFT_PAIR was set
   int pair_tx, pair_ty;  // pair tile (pair_geometry, once per slab); 0 x 0: none fits
   long pair_ntile;
+  double timeout_s;      // bound on a host wait for the compute stream while ipc peers are on
+                         // (env PFT_IPC_TIMEOUT, default 300 s; slab_wait)
   // per-stage timing: a ring of begin/end event pairs, so that kernels still running when the
   // host collects (the speculative stage 1) are picked up by a later collect
   hipEvent_t tev[6][PFT_TRING][2];
@@ -1837,7 +1840,56 @@ struct pft_slab {
   long tacc_n[6];
 };
 
+static double wall_s()
+{
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+// A dead or diverged ipc peer never raises the flag word the compute stream waits on
+// (hipStreamWaitValue64, pft_slab_halo_wait), so the stream would never drain.  On expiry of
+// s->timeout_s the slab raises its own flag words past every sequence number (on the side stream,
+// which nothing blocks): the compute stream drains -- its results are void -- and the caller gets
+// PFT_ERR_IPC_TIMEOUT, which RK_MPI_SA_solve reports as PFT_SOLVE_DEVICE_ERROR.
+static int slab_timed_out(pft_slab* s, const char* what)
+{
+  static const unsigned long long released[2] = {~0ULL >> 1, ~0ULL >> 1};
+  (void)hipMemcpyAsync(s->sig, released, sizeof(released), hipMemcpyHostToDevice, s->side);
+  (void)hipStreamSynchronize(s->side);
+  (void)hipStreamSynchronize(s->stream);
+  (void)hipGetLastError();
+  snprintf(g_err, sizeof(g_err), "%s: no halo from an ipc neighbour within %.0f s (PFT_IPC_TIMEOUT)", what,
+           s->timeout_s);
+  fprintf(stderr, "libpft: %s\n", g_err);
+  return PFT_ERR_IPC_TIMEOUT;
+}
+
+// the host waits for an event (or the whole compute stream when ev is null): unbounded with no ipc
+// peer, bounded by s->timeout_s with one
+static int slab_wait(pft_slab* s, hipEvent_t ev, const char* what)
+{
+  if (!s->peer[0].on && !s->peer[1].on) {
+    HIPCHK(ev ? hipEventSynchronize(ev) : hipStreamSynchronize(s->stream));
+    return 0;
+  }
+  const double t0 = wall_s();
+  for (long it = 0;; ++it) {
+    const hipError_t q = ev ? hipEventQuery(ev) : hipStreamQuery(s->stream);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) return fail(q, what);
+    if (it < 20000) {
+      __builtin_ia32_pause();
+    } else {
+      sched_yield();
+      if ((it & 1023) == 0 && wall_s() - t0 > s->timeout_s) return slab_timed_out(s, what);
+    }
+  }
+}
+
 extern "C" {
+
+int pft_slab_sync(pft_slab* s) { return s ? slab_wait(s, nullptr, "pft_slab_sync") : -2; }
 
 const char* pft_hip_last_error(void) { return g_err; }
 
@@ -1891,11 +1943,17 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
     // push inside the stage kernels 5-9% (its boundary workgroups finish last)
     const char* e = getenv("PFT_IPC_FUSED_PUSH");
     s->fused_push = e ? atoi(e) : 0;
+    // fault injection (tests/test_ipc_multiprocess.py): this slab never delivers its halo -- no
+    // put, no flag raise -- as a peer that died would not
+    const char* ed = getenv("PFT_IPC_DROP_PUTS");
+    s->drop_puts = ed ? atoi(ed) : 0;
     // pair kernels where the slab qualifies (pft_slab_pair_ok); env PFT_PAIR=0 turns them off (A/B)
     const char* ep = getenv("PFT_PAIR");
     s->pair_env = ep != nullptr;
     s->pair_on = ep ? atoi(ep) : 1;
     s->pair_ntile = pair_geometry(d->n1, d->n2, &s->pair_tx, &s->pair_ty);
+    const char* et = getenv("PFT_IPC_TIMEOUT");
+    s->timeout_s = (et && atof(et) > 0.0) ? atof(et) : 300.0;
   }
   const size_t bytes = sizeof(double) * (3 * (size_t)s->fs + 2 * (size_t)s->plane);
   hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
@@ -2017,8 +2075,7 @@ int pft_slab_upload_host(pft_slab* s, int which, const double* host_padded)
                         s->stream));
   pack_kernel<<<2048, 256, 0, s->stream>>>(s->staging, s->buf[which], s->d.n1, s->d.n2, s->d.n3, s->fs, s->S);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(s->stream));
-  return 0;
+  return slab_wait(s, nullptr, "upload");
 }
 
 int pft_slab_download_host(pft_slab* s, int which, double* host_padded)
@@ -2032,8 +2089,7 @@ int pft_slab_download_host(pft_slab* s, int which, double* host_padded)
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(host_padded, s->staging, sizeof(double) * 3 * (size_t)s->S, hipMemcpyDeviceToHost,
                         s->stream));
-  HIPCHK(hipStreamSynchronize(s->stream));
-  return 0;
+  return slab_wait(s, nullptr, "download");
 }
 
 }  // extern "C"
@@ -2506,16 +2562,22 @@ int pft_slab_eps_fetch(pft_slab* s, double* eps, int* nonfinite)
     s->eps_marked = 0;
     volatile unsigned long long* w = s->pub_ring + 2 * s->pub_slot;
     long spins = 0;
+    double t0 = 0.0;
     while (__atomic_load_n(&w[0], __ATOMIC_ACQUIRE) == PFT_PUB_SENTINEL ||
            __atomic_load_n(&w[1], __ATOMIC_ACQUIRE) == PFT_PUB_SENTINEL) {
       if (++spins < 200000) {
         __builtin_ia32_pause();
       } else if ((spins & 1023) == 0) {
-        // long wait: make sure the stream is alive (a fault ends here with its error)
+        // long wait: make sure the stream is alive (a fault ends here with its error), and that an
+        // ipc neighbour's halo has not been missing for longer than the slab's timeout
         const hipError_t q = hipStreamQuery(s->stream);
         if (q != hipSuccess && q != hipErrorNotReady) return fail(q, "hipStreamQuery (error norm poll)");
         if (q == hipSuccess && __atomic_load_n(&w[1], __ATOMIC_ACQUIRE) == PFT_PUB_SENTINEL)
           return fail(hipErrorUnknown, "error norm never published");
+        if (s->peer[0].on || s->peer[1].on) {
+          if (t0 == 0.0) t0 = wall_s();
+          else if (wall_s() - t0 > s->timeout_s) return slab_timed_out(s, "error norm poll");
+        }
         sched_yield();
       }
     }
@@ -2525,12 +2587,14 @@ int pft_slab_eps_fetch(pft_slab* s, double* eps, int* nonfinite)
     // read back on the side stream: work enqueued on the compute stream after the mark (the
     // speculative stage 1 of the next step) keeps running while the host decides
     s->eps_marked = 0;
-    HIPCHK(hipEventSynchronize(s->ev_eps));
+    int rc = slab_wait(s, s->ev_eps, "error norm event");
+    if (rc) return rc;
     s->host_scratch[0] = __atomic_load_n(&s->host_pub[0], __ATOMIC_ACQUIRE);
     s->host_scratch[1] = __atomic_load_n(&s->host_pub[1], __ATOMIC_ACQUIRE);
   } else {
     HIPCHK(hipMemcpyAsync(s->host_scratch, s->scratch, 16, hipMemcpyDeviceToHost, s->stream));
-    HIPCHK(hipStreamSynchronize(s->stream));
+    int rc = slab_wait(s, nullptr, "error norm read-back");
+    if (rc) return rc;
   }
   unsigned long long b = s->host_scratch[0];
   double v;
@@ -2863,6 +2927,23 @@ int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, lo
     p.on = 1;
     return 0;
   }
+  int mine = 0;
+  HIPCHK(hipGetDevice(&mine));
+  if (device != mine) {
+    // A neighbour on another GPU writes our ghost planes over xGMI.  Whether this GPU's L2 can
+    // still hold lines of a ghost plane from before that write (coarse-grained hipMalloc memory)
+    // has not been verified on hardware, and a stale line would silently corrupt the halo: refused
+    // unless explicitly enabled (use the RCCL transport across GPUs)
+    const char* e = getenv("PFT_IPC_CROSS_GPU");
+    if (!(e && atoi(e) == 1)) {
+      snprintf(g_err, sizeof(g_err),
+               "ipc neighbour on device %d, this slab on device %d: cross-GPU ipc halos are unverified "
+               "(set PFT_IPC_CROSS_GPU=1 to allow; the rccl transport is the supported one)",
+               device, mine);
+      fprintf(stderr, "libpft: %s\n", g_err);
+      return -2;
+    }
+  }
   const hipIpcMemHandle_t* h = (const hipIpcMemHandle_t*)handles;
   for (int b = 0; b <= PFT_BUF_COUNT; ++b) {
     void* ptr = nullptr;
@@ -2876,8 +2957,6 @@ int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, lo
   }
   p.n3 = n3;
   p.fs = fs;
-  int mine = 0;
-  HIPCHK(hipGetDevice(&mine));
   p.remote = device != mine;
   p.opened = 1;
   p.on = 1;
@@ -2911,6 +2990,7 @@ double* pft_slab_far(pft_slab* s, int which, int q, int side)
 int pft_slab_halo_put2(pft_slab* s, int role, int f0, int f1, int deep, unsigned long long seq)
 {
   if (role < 0 || role >= PFT_BUF_COUNT || f0 < 0 || f1 > 3 || f1 <= f0) return -2;
+  if (s->drop_puts) return 0;
   const int ph = s->phys[role];
   PutArgs a;
   memset(&a, 0, sizeof(a));
@@ -2944,6 +3024,7 @@ int pft_slab_halo_put2(pft_slab* s, int role, int f0, int f1, int deep, unsigned
 
 int pft_slab_halo_signal(pft_slab* s, unsigned long long seq)
 {
+  if (s->drop_puts) return 0;
   unsigned long long* slo = s->peer[0].on ? s->peer[0].sig + 1 : nullptr;   // below: its "from above"
   unsigned long long* shi = s->peer[1].on ? s->peer[1].sig + 0 : nullptr;   // above: its "from below"
   if (!slo && !shi) return 0;

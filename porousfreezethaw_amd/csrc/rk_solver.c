@@ -49,6 +49,10 @@ typedef struct {
 	int tstep;                  /* this attempted step's stages are timed (every opt_timing-th) */
 	int last_status;            /* raw status of the last device / communication failure */
 	int in_callback;            /* inside Service_Callback on the fused path (x is on the device) */
+	int rhs_failed;             /* sticky: a device evaluation of libpft's RHS on a host array failed
+	                               (f_generic_model01/2 cannot report it: the reference's f is void);
+	                               the host-staged loop checks it after every f() */
+	long fail_rhs_after, rhs_calls;   /* PFT_OPT_FAIL_RHS test hook */
 	pft_solver_stats stats;
 } solver_state;
 
@@ -160,6 +164,7 @@ int pft_solver_set_option(int opt, long value)
 		case PFT_OPT_ONE_STREAM: if(value < 0 || value > 2) return -2; R.opt_one_stream = (int)value; return 0;
 		case PFT_OPT_WAVE: if(value < 0) return -2; R.opt_wave = (int)value; return 0;
 		case PFT_OPT_LAZY_ALLOC: R.opt_lazy = value ? 1 : 0; return 0;
+		case PFT_OPT_FAIL_RHS: if(value < 0) return -2; R.fail_rhs_after = value; R.rhs_calls = 0; return 0;
 		case PFT_OPT_PAIR: if(value < 0 || value > 2) return -2; R.opt_pair = (int)value; return 0;
 		case PFT_OPT_RECOMPUTE:
 			R.opt_norecompute = value ? 0 : 1; if(R.slab) pft_slab_set_recompute(R.slab, !R.opt_norecompute); return 0;
@@ -598,8 +603,11 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	if(to_host) {
 		/* meta_f() returned a right-hand side that is not libpft's: carry on from t, h and the
 		   pending command with it, on the host-staged path (hybrid2.c:732 keeps integrating with
-		   the new f) */
+		   the new f) -- unless the step cap ended this call on that very step: then it returns 2
+		   like any capped call, and the next call (its prologue calls meta_f()) takes the
+		   host-staged path from the start */
 		R.device_valid = 0;
+		if(ret == 2) return ret;
 		B->t = t;
 		B->h = h;
 		return run_staged(system, f, B, command, max_steps_total > 0 ? max_steps_total - attempted : 0, flags);
@@ -618,11 +626,17 @@ int pft_solver_eval_rhs(FLOAT t, const FLOAT * w, FLOAT * dw)
 	/* f(t, w, dw) on host arrays: stage w into A0, exchange its boundary planes, K into K1 */
 	pft_comm * c = comm();
 	int rc;
-	if(!(rc = ensure_slab()) && !(rc = pft_slab_upload_host(R.slab, PFT_BUF_A0, w)) &&
+	if(R.fail_rhs_after > 0 && ++R.rhs_calls >= R.fail_rhs_after) {
+		R.fail_rhs_after = 0;
+		rc = -1000 - 999;                    /* as a hipError_t the runtime reports for a fault */
+	} else if(!(rc = ensure_slab()) && !(rc = pft_slab_upload_host(R.slab, PFT_BUF_A0, w)) &&
 	   !(pft_comm_size(c) > 1 && (rc = pft_comm_halo(c, PFT_BUF_A0, 0, 3))) &&
 	   !(rc = pft_slab_rhs(R.slab, PFT_BUF_A0, PFT_BUF_K1, t)))
 		rc = pft_slab_download_host(R.slab, PFT_BUF_K1, dw);
-	if(rc) R.last_status = rc;
+	if(rc) {
+		R.last_status = rc;
+		R.rhs_failed = 1;
+	}
 	return rc;
 }
 
@@ -677,7 +691,14 @@ static int staged_rhs(RK_RightHandSide f, double t, const double * d_in, double 
 	if(d_in) {
 		if((rc = pft_flat_d2h(host_in, d_in, R.max_n, NULL)) || (rc = pft_stream_sync(NULL))) return rc;
 	}
+	R.rhs_failed = 0;
 	f(t, host_in, R.h_k);
+	if(R.rhs_failed) {
+		/* libpft's own f failed on the device and left NaN in h_k: never let that pass as a step
+		   (the reference driver leaves NaN handling off, intertrack.c:2193) */
+		R.rhs_failed = 0;
+		return R.last_status <= -1000 ? R.last_status : -1;
+	}
 	if((rc = pft_flat_h2d(d_out, R.h_k, R.max_n, NULL))) return rc;
 	return 0;
 }

@@ -44,6 +44,18 @@ def main():
                        spec.get("mode", 0), Pm, nprocs=n, rank=rank, initial=ic, beads=beads, tau=1.0,
                        tau_min=info["tau_min"], delta=info["delta"], tile=spec.get("tile"))
     rows, states = [], []
+    if spec.get("raw_rc"):
+        # fault-injection runs: one pft_solve_ex call, its raw return code and timing recorded
+        import ctypes as C
+        import time
+        t0 = time.time()
+        rc = P.lib().pft_solve_ex(spec["times"][0], C.byref(sim.system), spec.get("steps", 0), 0)
+        el = time.time() - t0
+        status = P.lib().pft_solver_last_status()
+        sim.close()
+        P.comm_destroy(comm)
+        np.savez(f"{spec['out']}.{rank}.npz", rc=rc, status=status, seconds=el)
+        return
     for T in spec["times"]:
         if spec.get("steps"):
             rc = sim.solve_ex(T, spec["steps"], 0)

@@ -151,3 +151,99 @@ def test_host_staged_path_keeps_the_ghosts_f_wrote():
                     O.ptr(x), C.byref(steps), C.byref(total), 0, O.EXCHANGE_FN(), O.ALLREDUCE_FN(), None)
     assert np.array_equal(sim.x, x)
     sim.close()
+
+
+def test_device_failure_in_own_rhs_on_host_path_is_a_device_error():
+    """libpft's own f (f_generic_model01) called by the host-staged path -- a DDLBF_Rearrange
+    callback keeps the solve off the fused path (hybrid2.c:726-729) -- whose device evaluation
+    fails (PFT_OPT_FAIL_RHS): the solve must return PFT_SOLVE_DEVICE_ERROR, not accept the NaN
+    state f leaves behind (the reference driver runs with NaN handling off, intertrack.c:2193)"""
+    sim, meta, A, Pm, info = _g20_sim()
+
+    @P.REARRANGE_FN
+    def same(n):
+        return n
+
+    sim.system.DDLBF_Rearrange = C.cast(same, C.c_void_p).value
+    L = sim.lib
+    try:
+        assert L.pft_solver_set_option(P.PFT_OPT_FAIL_RHS, 7) == 0    # the 2nd step's second stage
+        rc = L.RK_MPI_SA_solve(meta["traj_times"][0], C.byref(sim.system))
+        assert sim.stats().path == 2
+        assert rc == P.PFT_SOLVE_DEVICE_ERROR
+        assert L.pft_solver_last_status() <= -1000
+        assert sim.system.steps_total == 1
+    finally:
+        L.pft_solver_set_option(P.PFT_OPT_FAIL_RHS, 0)
+        sim.close()
+
+
+def test_rearrange_callback_host_path_matches_golden():
+    """the same host-staged run with libpft's own f and no failure ends on golden g20"""
+    sim, meta, A, Pm, info = _g20_sim()
+
+    @P.REARRANGE_FN
+    def same(n):
+        return n
+
+    sim.system.DDLBF_Rearrange = C.cast(same, C.c_void_p).value
+    T = meta["traj_times"][0]
+    rc = sim.solve(T)
+    ref = meta["traj_m0"][0]
+    assert sim.stats().path == 2
+    assert (sim.t, sim.system.steps, sim.system.steps_total, rc) == \
+        (float.fromhex(ref[0]), ref[2], ref[3], ref[4])
+    assert np.array_equal(sim.interior(), A["traj_m0_state0"])
+    sim.close()
+
+
+def test_meta_f_switch_on_the_capped_step_returns_2():
+    """meta_f switches to a foreign RHS on the very attempted step that reaches the cap of
+    pft_solve_ex: the call returns 2 (not a run to final_time), and the next call continues on
+    the host-staged path to the reference trajectory"""
+    # the attempted-step count at which the 10th step is accepted (uninterrupted device run)
+    probe = []
+
+    @P.SERVICE_FN
+    def cnt(final, s):
+        probe.append(s.contents.steps_total)
+        return 0
+
+    sim2, meta, A, Pm, info = _g20_sim(tile=32)
+    sim2.system.Service_Callback = C.cast(cnt, C.c_void_p).value
+    T = meta["traj_times"][0]
+    sim2.solve(T)
+    sim2.close()
+    sim, meta, A, Pm, info = _g20_sim(tile=32)
+    g = O.make_grid(info)
+    OL = O.lib()
+    dev_f = sim.lib.mf_single()
+    accepted = []
+
+    @P.RHS_FN
+    def host_f(t, w, dw):
+        OL.pft_or_rhs(C.byref(g), O.ptr(Pm), 0, t, w, dw)
+
+    host_addr = C.cast(host_f, C.c_void_p).value
+
+    @P.META_FN
+    def meta_f():
+        return dev_f if len(accepted) < 10 else host_addr
+
+    @P.SERVICE_FN
+    def cb(final, s):
+        accepted.append(s.contents.steps)
+        return 0
+
+    sim.system.meta_f = C.cast(meta_f, C.c_void_p).value
+    sim.system.Service_Callback = C.cast(cb, C.c_void_p).value
+    cap = probe[9]                              # attempted steps when the 10th step is accepted
+    rc = sim.solve_ex(T, cap, 0)
+    assert rc == 2 and sim.system.steps_total == cap and sim.system.steps == 10
+    rc = sim.solve(T)
+    ref = meta["traj_m0"][0]
+    assert sim.stats().path == 2
+    assert (sim.t, sim.system.steps, sim.system.steps_total, rc) == \
+        (float.fromhex(ref[0]), ref[2], ref[3], ref[4])
+    assert np.array_equal(sim.interior(), A["traj_m0_state0"])
+    sim.close()

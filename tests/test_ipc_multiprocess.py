@@ -34,16 +34,17 @@ def need_gpu():
         pytest.fail("no HIP device: the gpu tests must run on an MI355X (no CPU fallback exists)")
 
 
-def _run_ranks(tmp_path, nranks, timeout=240, push=None, **spec):
+def _run_ranks(tmp_path, nranks, timeout=240, push=None, rank_env=None, ipc_timeout="120", **spec):
     spec = dict(spec, nranks=nranks, shm=f"/pft_test_{os.getpid()}_{uuid.uuid4().hex[:12]}",
                 out=str(tmp_path / "rank"))
     path = tmp_path / "spec.json"
     path.write_text(json.dumps(spec))
-    env = dict(os.environ, PFT_IPC_TIMEOUT="120")
+    env = dict(os.environ, PFT_IPC_TIMEOUT=ipc_timeout)
     if push is not None:
         env["PFT_IPC_FUSED_PUSH"] = str(push)     # 1: the stage kernels store the boundary planes
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "_ipc_worker.py"), str(path), str(r)],
-                              env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(nranks)]
+                              env=dict(env, **((rank_env or {}).get(r, {}))), stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT) for r in range(nranks)]
     outs = []
     try:
         for p in procs:
@@ -140,3 +141,18 @@ def test_ipc_self_exchange_equals_reference(tile):
         sim.close()
     finally:
         P.comm_destroy(comm)
+
+
+def test_lost_ipc_halo_ends_in_device_error_not_a_hang(tmp_path):
+    """rank 1 never delivers its halo (fault injection PFT_IPC_DROP_PUTS=1: its puts and flag
+    raises are skipped), so rank 0's compute stream blocks on a flag word that never comes.  Every
+    host wait of the slab is bounded by PFT_IPC_TIMEOUT (here 5 s): both ranks return
+    PFT_SOLVE_DEVICE_ERROR and exit, with the raw status an ipc timeout (-5000 host round,
+    -5002 device halo) -- not a hang"""
+    res = _run_ranks(tmp_path, 2, timeout=180, case="g20", times=[36.0], raw_rc=True, ipc_timeout="5",
+                     rank_env={1: {"PFT_IPC_DROP_PUTS": "1"}})
+    for r in res:
+        assert int(r["rc"]) == P.PFT_SOLVE_DEVICE_ERROR
+        assert int(r["status"]) in (-5000, -5002)
+        assert float(r["seconds"]) < 60
+    assert int(res[0]["status"]) == -5002            # rank 0 waited on the device flag
