@@ -22,6 +22,12 @@ Cases (SURVEY.md section 4.2 KATs 1-4):
   g100     BASELINE configs[0]: default Params at grid_nodes 100 (50x50x100): parameters, the
            SHA-256 of the IC and of a mode-0 trajectory to two snapshot times (checked identical
            on 2 ranks), plus the middle and top z-planes of each state (a state is 6 MB).
+  g200     BASELINE configs[1]: grid_nodes 200 (100x100x200), the same record for calc_mode 0 to
+           t = 0.01 and 0.03 s (35 and 65 attempted steps) and calc_mode 1 to t = 0.03 s; run on
+           8 MPI ranks and checked identical on 3.
+  g400     BASELINE configs[2]: grid_nodes 400 (200x200x400, 16 M cells), calc_mode 0 to
+           t = 0.002 and 0.005 s (about 45 and 67 attempted steps); run on 8 MPI ranks and checked
+           identical on 5 (about 3 minutes of the build container's 8 cores).
 
     python tests/golden/gen_golden.py [case ...]     (default: all)
 """
@@ -200,6 +206,48 @@ def case_g100():
     return arrays, meta
 
 
+def case_large(name, gn, runs, nranks, check_ranks):
+    """a full-size BASELINE grid: per calc_mode, the reference's trajectory to `times` on nranks
+    MPI ranks (re-checked on check_ranks), stored as digests plus the middle and top planes"""
+    arrays, meta = {}, {"case": name, "source": f"reference Params, grid_nodes {gn}",
+                        "mpi_ranks": nranks, "checked_on_ranks": check_ranks}
+    for mode, times in runs:
+        w = Work({"grid_nodes": gn, "calc_mode": mode})
+        try:
+            out = w.run(nranks, "setup", timeout=3600)
+            p = read_params(out)
+            shape = (3, p["n3"], p["n2"], p["n1"])
+            ic = load(os.path.join(out, "ic.f64"), shape)
+            if mode == runs[0][0]:
+                meta["params"] = hexify(p)
+            meta[f"m{mode}_params"] = hexify(p)
+            meta[f"m{mode}_ic_sha256"] = sha256(ic)
+            icp = os.path.join(w.dir, "ic.f64")
+            ic.tofile(icp)
+            o = w.run(nranks, "solve", icp, 0.0, 1.0, *times, timeout=3600)
+            tm, st = traj(o, len(times), shape)
+            o2 = w.run(check_ranks, "solve", icp, 0.0, 1.0, *times, timeout=3600)
+            tm2, st2 = traj(o2, len(times), shape)
+            assert tm == tm2 and all(np.array_equal(a, b) for a, b in zip(st, st2)), "decomposition invariance"
+            meta[f"traj_m{mode}_times"] = times
+            meta[f"traj_m{mode}"] = tm
+            meta[f"traj_m{mode}_sha256"] = [sha256(x) for x in st]
+            for i, x in enumerate(st):
+                arrays[f"traj_m{mode}_state{i}_mid"] = x[:, shape[1] // 2]
+                arrays[f"traj_m{mode}_state{i}_top"] = x[:, -1]
+        finally:
+            w.close()
+    return arrays, meta
+
+
+def case_g200():
+    return case_large("g200", 200, [(0, [0.01, 0.03]), (1, [0.03])], 8, 3)
+
+
+def case_g400():
+    return case_large("g400", 400, [(0, [0.002, 0.005])], 8, 5)
+
+
 def traj_ext(out, ncalls, shape):
     """solvex rows: t, h, steps, steps_total, rc, check_NAN; cb.txt rows: steps, t, h"""
     rows = [l.split() for l in open(os.path.join(out, "traj.txt"))]
@@ -315,7 +363,8 @@ def case_ragged():
 def main():
     if not os.path.exists(PFT_REF):
         sys.exit("build the reference harness first: make -C oracle ref")
-    cases = {"g20": case_g20, "ragged": case_ragged, "g100": case_g100, "ctl": case_ctl}
+    cases = {"g20": case_g20, "ragged": case_ragged, "g100": case_g100, "ctl": case_ctl, "g200": case_g200,
+             "g400": case_g400}
     for name in sys.argv[1:] or list(cases):
         arrays, meta = cases[name]()
         name = meta["case"]
