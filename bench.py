@@ -103,15 +103,6 @@ def parse():
     ap.add_argument("--timing-steps", type=int, default=30,
                     help="attempted steps of the separate, untimed pass that measures the stage kernels with "
                          "HIP events (roofline); 0 = none")
-    ap.add_argument("--two-stream", action="store_true",
-                    help="N>1 stage pipeline on two streams (boundary launch and exchange on the comm stream "
-                         "beside the interior sweep) instead of the default one-stream pipeline")
-    ap.add_argument("--comm-boundary", action="store_true",
-                    help="N>1 stage pipeline: boundary launch and exchange on the comm stream, the interior "
-                         "sweep waiting for the boundary launch (PFT_OPT_ONE_STREAM 2)")
-    ap.add_argument("--wave", type=int, default=0,
-                    help="W > 0: a step's five stages as a skewed z-wavefront of W-plane launches "
-                         "(PFT_OPT_WAVE; N = 1)")
     ap.add_argument("--no-parity", action="store_true",
                     help="N > 1: skip the decomposition-invariance check (rank 0 re-runs the same attempted "
                          "steps on one slab of its own GPU and compares every rank's state bit for bit)")
@@ -157,8 +148,6 @@ def main():
             comm = make_comm(L, a.transport, 1, 0, dev, None)
             assert L.pft_comm_set_self_exchange(comm, 1) == 0
     L.pft_solver_set_option(P.PFT_OPT_DEVICE, dev)
-    L.pft_solver_set_option(P.PFT_OPT_ONE_STREAM, 0 if a.two_stream else (2 if a.comm_boundary else 1))
-    L.pft_solver_set_option(P.PFT_OPT_WAVE, a.wave)
 
     def barrier():
         if dist is not None:
@@ -235,8 +224,7 @@ def main():
     roof = None
     if not a.no_timing and stats.stage_n[1] > 0:
         per = {}
-        # wavefront (--wave): stages 2..5 are timed per launch, nl[s] launches of W planes per step
-        nl = wave_launches(sim.grid.n3, a.wave) if a.wave and world == 1 else {s: 1 for s in range(1, 6)}
+        nl = {s: 1 for s in range(1, 6)}
         for s in range(1, 6):
             if stats.stage_n[s] == 0:
                 continue                                                 # a pair's first stage
@@ -248,7 +236,7 @@ def main():
         achieved = byts / (ms * 1e-3) / 1e9
         traffic, traffic_src, valu_frac, f64 = None, None, None, {}
         pmc = os.path.join(REPO, "profiles", "pmc_summary.json")
-        if os.path.exists(pmc) and not a.wave:
+        if os.path.exists(pmc):
             try:
                 ps = json.load(open(pmc))
                 key = f"{'pair' if pairs else 'stage'}{dom}_gl{int(a.gl_static)}_{n1}x{n2}x{sim.grid.n3}_m{a.mode}"
@@ -312,8 +300,6 @@ def main():
                    "host_boundary": a.host_boundary, "self_exchange": a.self_exchange,
                    "transport": (a.transport if (world > 1 or a.self_exchange) else None),
                    "service_callback": a.callback,
-                   "pipeline": ("two-stream" if a.two_stream else "comm-boundary" if a.comm_boundary
-                                else "one-stream"), "wave": a.wave,
                    "gl_store_skipped": gl_keep, "pair_kernels": pairs,
                    "tiles": ({str(k): ("cache" if v[0] == 0 else f"{2 * v[1]}x{v[2]} cells")
                               for k, v in geo.items()} if geo else None)},
@@ -373,9 +359,13 @@ def slab_digest(sim):
     """this rank's trajectory position and the SHA-256 of its interior (u, p, gl planes of the slab)"""
     sim.download()
     g = sim.grid
+    x = sim.interior()
+    if os.environ.get("PFT_BENCH_PARITY_PERTURB") == str(g.rank):
+        # diagnostic: one value of this rank's state off by one ulp, so that the check must fail
+        x.reshape(-1)[x.size // 2] = np.nextafter(x.reshape(-1)[x.size // 2], np.inf)
     return {"t": float(sim.t).hex(), "h": float(sim.h).hex(), "steps": int(sim.system.steps),
             "steps_total": int(sim.system.steps_total), "first_row": int(g.first_row), "n3": int(g.n3),
-            "sha256": hashlib.sha256(sim.interior().tobytes()).hexdigest()}
+            "sha256": hashlib.sha256(x.tobytes()).hexdigest()}
 
 
 def parity_check(ranks, calls, a, base, dims, Ls, beads, final_time, dev):
@@ -451,16 +441,6 @@ def workload(grid_nodes, world, shape="cube", literal_cube=False, mode=0, domain
     base = PR.default_params(grid_nodes=grid_nodes, calc_mode=mode, L=Lc)
     return (grid_nodes, base, (base["n1"], base["n2"], base["n3"] * world),
             (base["L1"], base["L2"], base["L3"] * world))
-
-
-def wave_launches(n3, w):
-    """launches per step of each stage in the wavefront schedule (rk_solver.c wave_stages);
-    stage 1 is the speculative launch, one per step"""
-    nl = {1: 1}
-    for s in range(2, 6):
-        nl[s] = sum(1 for c in range(0, (n3 + 4) // w + 2)
-                    if c * w - 4 < n3 and max(0, c * w - (s - 1)) < min(n3, (c + 1) * w - (s - 1)))
-    return nl
 
 
 def kernel_name(stage, a, rc_path, n1, pairs=False):

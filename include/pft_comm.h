@@ -80,10 +80,6 @@ int pft_comm_attach(pft_comm * c, pft_slab * s);
    No-ops for a single rank. */
 int pft_comm_halo_start(pft_comm * c, int buf, int f0, int f1);
 int pft_comm_halo_finish(pft_comm * c);
-/* the exchange enqueued on the slab's communication stream behind the work already there (the
-   boundary planes of the two-stream stage pipeline, rk_solver.c do_stage): nothing to finish,
-   later work on the comm stream follows it in stream order */
-int pft_comm_halo_enqueue_comm(pft_comm * c, int buf, int f0, int f1);
 int pft_comm_halo(pft_comm * c, int buf, int f0, int f1);   /* start + finish */
 /* the pair kernels' two-plane halo: planes 1, 2 and n3-1, n3 into the neighbours' ghost and far
    ghost planes (pft_slab_far), start + finish; needs n3 >= 2 on every slab */

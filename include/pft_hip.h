@@ -78,18 +78,17 @@ const pft_slab_desc * pft_slab_get_desc(const pft_slab * s);
 /* planes per workgroup z-march (tuning knob); 0 (default) = automatic: the fewest planes per
    workgroup that keep the whole launch resident in one round (occupancy x CUs / tiles chunks) */
 int pft_slab_set_kz(pft_slab * s, int kz);
-/* stage kernel flavour: 32 or 16 = LDS-tiled kernel with 64x8 / 32x16 cell tiles (n1 even);
-   1 (default) = automatic: the cache kernel for slabs too small to fill the GPU with tiles, else
-   the fused kernel with a tile fitted to n1 x n2 (the aux-array kernel: 32x16 for stages 1-2,
-   64x8 for 3-5); 2 = as 1 at any slab size; 0 = cache-based kernel (any n1; also used
-   automatically for odd n1) */
+/* stage kernel flavour: 32 or 16 = the fused LDS-tiled kernel with 64x8 / 32x16 cell tiles (n1
+   even); 1 (default) = automatic: the fused kernel with a tile fitted to n1 x n2, or the cache
+   kernel where that tile would leave most lanes idle; 2 = the fitted tile at any size; 0 = the
+   cache-based kernel (any n1; also used for odd n1 and for the aux-array path) */
 int pft_slab_set_tile(pft_slab * s, int wx);
-/* the kernel flavour (0 cache, 1 LDS tile with aux arrays, 2 fused recompute) and tile (wx cell
-   pairs x ty rows; 0 x 0 for the cache kernel) that stage 1..5 launches on this slab */
+/* the kernel flavour (0 cache, 2 fused recompute; 1 is retired) and tile (wx cell pairs x ty
+   rows; 0 x 0 for the cache kernel) that stage 1..5 launches on this slab */
 int pft_slab_tile_geometry(const pft_slab * s, int stage, int * wx, int * ty);
 /* 1 (default): the tiled kernels rebuild every stage input from x and the K's inside the
-   stencil (no aux arrays: 54 instead of 72 doubles of traffic per cell-step, bit-identical);
-   0: the reference's aux arrays are materialised between stages */
+   stencil (no aux arrays: 39 instead of 72 doubles of traffic per cell-step, bit-identical);
+   0: the reference's aux arrays are materialised between stages (cache kernel) */
 int pft_slab_set_recompute(pft_slab * s, int on);
 /* 1: X and XN hold the same gl field and no gl value is -0.0 or NaN (the caller checked), so
    stage 5 need not store gl's x(t+h) = x + coef*0.0 (== x); cleared by every upload */
@@ -103,15 +102,9 @@ int pft_slab_stage_output(const pft_slab * s, int stage);
    path, where gl's K's are the literal zeros of dgl (equation.c:731) and never stored */
 int pft_slab_stage_fields(const pft_slab * s, int stage);
 
-/* N > 1 stage pipeline on two streams: stage launches go to the comm stream while `on` is set
-   (the boundary planes, then their exchange, beside the interior sweep on the compute stream);
-   pft_slab_order(s, 0): the comm stream waits for the compute stream's work so far, (s, 1): the
-   compute stream waits for the comm stream's */
-int pft_slab_launch_on_comm(pft_slab * s, int on);
+/* stream order between the slab's two streams: pft_slab_order(s, 0): the comm stream waits for
+   the compute stream's work so far, (s, 1): the compute stream waits for the comm stream's */
 int pft_slab_order(pft_slab * s, int comm_first);
-/* wait = 0: mark the boundary launch just enqueued on the comm stream; wait = 1: the compute
-   stream waits for the last marked boundary launch (not for anything enqueued after it) */
-int pft_slab_boundary_event(pft_slab * s, int wait);
 
 /* host layout (reference padded, ghost thickness 2) <-> device layout, on the compute stream */
 int pft_slab_upload_host(pft_slab * s, int which, const double * host_padded);
@@ -229,9 +222,6 @@ int pft_slab_halo_put2(pft_slab * s, int role, int f0, int f1, int deep, unsigne
 double * pft_slab_far(pft_slab * s, int which, int q, int side);
 /* raise the neighbours' flags to `seq` behind the work on the compute stream (halo_put calls it) */
 int pft_slab_halo_signal(pft_slab * s, unsigned long long seq);
-/* 1 when the last stage launch already stored the boundary planes of buffer `role` into the
-   neighbours' ghost planes (the fused kernel does, with neighbours set); clears the mark */
-int pft_slab_take_pushed(pft_slab * s, int role);
 int pft_slab_halo_wait(pft_slab * s, unsigned long long seq);
 /* The host waits for the compute stream.  With ipc neighbours attached every host wait of the
    slab (this one, up/download, the error-norm fetch) is bounded by PFT_IPC_TIMEOUT seconds

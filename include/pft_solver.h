@@ -52,15 +52,8 @@ enum {
 	                           cache-based kernel (pft_slab_set_tile) */
 	PFT_OPT_RECOMPUTE = 6,  /* 1 (default): rebuild stage inputs from x and the K's inside the
 	                           stencil, 0: materialise the aux arrays (pft_slab_set_recompute) */
-	PFT_OPT_ONE_STREAM = 7, /* N > 1 stage pipeline: 1 (default) = one compute stream (boundary
-	                           launch, the exchange on the comm stream beside the interior sweep,
-	                           wait); 0 = two streams (boundary launch and exchange on the comm
-	                           stream beside the interior sweep); 2 = boundary launch and exchange
-	                           on the comm stream, the interior sweep waiting for the launch */
-	PFT_OPT_WAVE = 8,       /* one slab, fused path: W > 0 runs a step's five stages as a skewed
-	                           z-wavefront of W-plane launches (chunk c: stage s on planes
-	                           [cW - s + 1, (c+1)W - s + 1)), so each K is read back while it is
-	                           still in the Infinity Cache; 0 (default) = one launch per stage */
+	/* 7, 8: retired (the two-stream / comm-boundary N > 1 orders and the z-wavefront stage
+	   schedule, measured slower: DESIGN.md section 8) */
 	PFT_OPT_LAZY_ALLOC = 9, /* 1: RK_MPI_SA_init only checks its arguments and the device buffers
 	                           are allocated by the first solve (host-only checks of the ABI);
 	                           0 (default): RK_MPI_SA_init allocates them, as hybrid2.c:101-112
@@ -69,7 +62,8 @@ enum {
 	                           inside stage B's stencil, never stored -- 21 instead of 39 doubles
 	                           per cell-step, bit-identical): 1 (default) = on slabs of at least
 	                           16 Ki cells per CU (4 M cells on MI355X), 2 = on any slab they fit,
-	                           0 = one launch per stage */,
+	                           0 = one launch per stage */
+	,
 	PFT_OPT_FAIL_RHS = 11   /* test hook: N > 0 makes the N-th device evaluation of libpft's own
 	                           right-hand side on a host array (f_generic_model01/2 called by the
 	                           host-staged path) fail as a device fault would; 0 (default) off */

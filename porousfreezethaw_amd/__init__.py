@@ -28,8 +28,6 @@ DELTA_LOCAL, DELTA_GLOBAL = 0, 1
 RKA_CMD_FINISHED = 8
 PFT_SOLVE_KEEP_DEVICE, PFT_SOLVE_REUSE_DEVICE = 1, 2
 PFT_OPT_GL_STATIC, PFT_OPT_KZ, PFT_OPT_DEVICE, PFT_OPT_TIMING, PFT_OPT_TILE, PFT_OPT_RECOMPUTE = 1, 2, 3, 4, 5, 6
-PFT_OPT_ONE_STREAM = 7
-PFT_OPT_WAVE = 8
 PFT_OPT_LAZY_ALLOC = 9
 PFT_OPT_PAIR = 10
 PFT_OPT_FAIL_RHS = 11
@@ -57,7 +55,7 @@ class RK_MPI_S_SOLUTION(C.Structure):
 
 
 SERVICE_FN = C.CFUNCTYPE(C.c_int, C.c_double, C.POINTER(RK_MPI_S_SOLUTION))
-REARRANGE_FN = C.CFUNCTYPE(C.POINTER(RK_MEM_DIST), C.POINTER(RK_MEM_DIST))
+REARRANGE_FN = C.CFUNCTYPE(C.c_void_p, C.c_void_p)   # RK_MEM_DIST* (*)(RK_MEM_DIST*)
 RK_MPI_S_SOLUTION._fields_ = [
     ("n", C.POINTER(RK_MEM_DIST)), ("t", C.c_double), ("x", C.POINTER(C.c_double)),
     ("meta_f", C.c_void_p), ("h", C.c_double), ("h_min", C.c_double), ("delta", C.c_double),

@@ -403,14 +403,12 @@ int pft_comm_attach(pft_comm* c, pft_slab* s)
 
 static void loop_barrier(pft_comm* c) { pthread_barrier_wait(&c->grp->bar); }
 
-static int halo_start(pft_comm* c, int buf, int f0, int f1, bool on_comm, bool deep = false)
+static int halo_start(pft_comm* c, int buf, int f0, int f1, bool deep = false)
 {
   if (!pft_comm_splits(c)) return 0;
   pft_slab* s = c->slab;
   if (!s) return -2;
-  // on_comm: the boundary planes were written on the comm stream itself (two-stream stage
-  // pipeline), so the exchange follows them in stream order with no handshake
-  hipStream_t st = (hipStream_t)(on_comm ? pft_slab_comm_stream(s) : pft_slab_stream(s));
+  hipStream_t st = (hipStream_t)pft_slab_stream(s);
   const size_t plane = pft_slab_plane(s), fs = pft_slab_field_stride(s);
   const int n3 = pft_slab_nz(s);
   double* b = pft_slab_buffer(s, buf);
@@ -422,16 +420,13 @@ static int halo_start(pft_comm* c, int buf, int f0, int f1, bool on_comm, bool d
     // stream-ordered on the compute stream: put (boundary planes into the neighbours' ghost
     // planes, then their flags), then wait for our own flags
     const unsigned long long seq = ++c->dseq;
-    int rc = (!deep && pft_slab_take_pushed(s, buf)) ? pft_slab_halo_signal(s, seq)
-                                                     : pft_slab_halo_put2(s, buf, f0, f1, deep ? 1 : 0, seq);
+    int rc = pft_slab_halo_put2(s, buf, f0, f1, deep ? 1 : 0, seq);
     return rc ? rc : pft_slab_halo_wait(s, seq);
   }
   if (c->kind == KIND_RCCL) {
     hipStream_t cs = (hipStream_t)pft_slab_comm_stream(s);
-    if (!on_comm) {
-      HCHK(hipEventRecord(c->ev_ready, st));
-      HCHK(hipStreamWaitEvent(cs, c->ev_ready, 0));
-    }
+    HCHK(hipEventRecord(c->ev_ready, st));
+    HCHK(hipStreamWaitEvent(cs, c->ev_ready, 0));
     NCCLCHK(ncclGroupStart());
     // deep: also the second planes into / from the far ghost planes; per peer the sends and the
     // peer's receives pair up in the same order (field by field: ghost plane, then far plane)
@@ -455,10 +450,8 @@ static int halo_start(pft_comm* c, int buf, int f0, int f1, bool on_comm, bool d
       }
     }
     NCCLCHK(ncclGroupEnd());
-    if (!on_comm) {
-      HCHK(hipEventRecord(c->ev_done, cs));
-      c->pending = 1;
-    }
+    HCHK(hipEventRecord(c->ev_done, cs));
+    c->pending = 1;
     return 0;
   }
   // loopback: pull the neighbours' boundary planes into our ghost planes
@@ -489,8 +482,7 @@ static int halo_start(pft_comm* c, int buf, int f0, int f1, bool on_comm, bool d
   return 0;
 }
 
-int pft_comm_halo_start(pft_comm* c, int buf, int f0, int f1) { return halo_start(c, buf, f0, f1, false); }
-int pft_comm_halo_enqueue_comm(pft_comm* c, int buf, int f0, int f1) { return halo_start(c, buf, f0, f1, true); }
+int pft_comm_halo_start(pft_comm* c, int buf, int f0, int f1) { return halo_start(c, buf, f0, f1); }
 
 int pft_comm_halo_finish(pft_comm* c)
 {
@@ -500,11 +492,11 @@ int pft_comm_halo_finish(pft_comm* c)
   return 0;
 }
 
-int pft_comm_halo_start_deep(pft_comm* c, int buf, int f0, int f1) { return halo_start(c, buf, f0, f1, false, true); }
+int pft_comm_halo_start_deep(pft_comm* c, int buf, int f0, int f1) { return halo_start(c, buf, f0, f1, true); }
 
 int pft_comm_halo_deep(pft_comm* c, int buf, int f0, int f1)
 {
-  int rc = halo_start(c, buf, f0, f1, false, true);
+  int rc = halo_start(c, buf, f0, f1, true);
   return rc ? rc : pft_comm_halo_finish(c);
 }
 

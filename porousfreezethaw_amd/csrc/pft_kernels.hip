@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -30,72 +31,12 @@
 
 #pragma clang fp contract(off)
 
-#define PFT_BLOCK 256
-// threads per workgroup of the fused stage kernel.  A/B: 512 (25 x 20-pair tiles, a third fewer
-// halo loads) measured 3-5% slower at 400^3 -- one workgroup per CU where 256 fit two to four
-#ifndef PFT_FBLOCK
-#define PFT_FBLOCK 256
-#endif
+#define PFT_BLOCK 256      // threads per workgroup of the cache kernel (merson_stage)
+#define PFT_FBLOCK 256     // ... of the fused stage kernel (merson_fused).  A/B: 512 (25 x 20-pair
+                           // tiles, a third fewer halo loads) measured 3-5% slower at 400^3 -- one
+                           // workgroup per CU where 256 fit two to four
 #define PFT_TRING 8
 #define PFT_PUB_SLOTS 64
-
-// recompute path: the gl components of K1..K4 are the literal zeros of dgl (equation.c:731,874),
-// not arrays in HBM (42 instead of 54 doubles per cell-step, bit-identical).  An A/B build with
-// -DPFT_GLK_LITERAL=0 materialises them as the reference does.
-#ifndef PFT_GLK_LITERAL
-#define PFT_GLK_LITERAL 1
-#endif
-// stage 5 of the recompute kernel keeps the combine operands of planes k and k+1 in registers
-// (measured 0.52 vs 0.65 ms at 400^3: re-loading them one plane later misses the 4 MiB L2)
-#ifndef PFT_S5_RELOAD
-#define PFT_S5_KEEP 1
-#endif
-// minimum waves per SIMD of the fused stage kernels 1-4 (stage 5 keeps ~250 VGPRs live: capped
-// at 256 so that two waves fit)
-#ifdef PFT_S5_KEEP
-#define PFT_S5_WAVES2 1   // stage 5 keeps two planes of combine operands: 2 waves per SIMD
-#else
-#define PFT_S5_WAVES2 0
-#endif
-#ifndef PFT_S5_GLZERO
-#define PFT_S5_GLZERO 1
-#endif
-#ifndef PFT_S5_FACE
-#define PFT_S5_FACE PFT_GLK_LITERAL
-#endif
-// stages with the two-deep z pipeline.  Measured at 400^3 (A/B, same box): faithful stages 3-4
-// 0.258 vs 0.288 / 0.296 ms once gl's K's became literals (operands as few as gl_static's); with
-// the tiles fitted to n1 (25 x 10 pairs) stage 1 0.158 vs 0.166 ms (148 VGPRs, 3 waves instead of
-// 4) and stage 2 0.217 vs 0.222 (182 VGPRs, 2 waves)
-// stage 5 skips storing gl's x(t+h) when XN already holds it (pft_slab_set_gl_keep); 0 = always store
-#ifndef PFT_GL_KEEP
-#define PFT_GL_KEEP 1
-#endif
-#ifndef PFT_DEEP_MASK
-#define PFT_DEEP_MASK ((1 << 1) | (1 << 2) | (1 << 3) | (1 << 4))
-#endif
-#ifndef PFT_DEEP_ALL
-#define PFT_DEEP_ALL PFT_GLK_LITERAL
-#endif
-#ifndef PFT_FUSED_WAVES
-#define PFT_FUSED_WAVES 3
-#endif
-#ifndef PFT_COMM_HIPRIO
-#define PFT_COMM_HIPRIO 1
-#endif
-#ifndef PFT_KUNROLL
-#define PFT_KUNROLL 1
-#endif
-// recompute path: stage 2 stores S = K1 + K2 (the sum stage 3's input combine forms,
-// hybrid2.c:408, same operands) in place of K2, so stage 3 reads x and S instead of x, K1, K2
-#ifndef PFT_K12_SUM
-#define PFT_K12_SUM 1
-#endif
-// stage 2 re-loads K1 of plane k for the sum (loaded one plane earlier: an L2 hit) instead of
-// keeping it in registers
-#ifndef PFT_K12_RELOAD
-#define PFT_K12_RELOAD 0
-#endif
 
 static __thread char g_err[256];
 
@@ -140,12 +81,6 @@ __device__ __forceinline__ void rhs_cell(const pft_consts& c, const Col& u, cons
 {
   // un = u + u_noise (equation.c:676,687); only the reaction terms see the noise
   const double pc = p.c, gc = g.c, uc = u.c;
-#ifdef PFT_ABLATE_RHS
-  // diagnostic build only (never shipped): same loads and stores, trivial arithmetic
-  du = ((u.xm + u.xp) + (u.ym + u.yp)) + ((u.zm + u.zp) + un) + gc;
-  dp = ((p.xm + p.xp) + (p.ym + p.yp)) + ((p.zm + p.zp) + pc) + (g.xm + g.xp + g.ym + g.yp + g.zm + g.zp);
-  return;
-#endif
   const double rho = gc * c.rho_g + (1.0 - gc) * (pc * c.rho_i + (1.0 - pc) * c.rho_w);
   const double cp = gc * c.cp_g + (1.0 - gc) * (pc * c.cp_i + (1.0 - pc) * c.cp_w);
   const double wi = fmax(0.0, 1.0 - c.zeta * gc);
@@ -219,14 +154,6 @@ __device__ __forceinline__ void rhs_cell_f(const pft_consts& c, const Col& u, co
 {
   constexpr bool FLUX = MODE != 10 && MODE != 11;
   const double pc = p.c, gc = g.c, uc = u.c;
-#ifdef PFT_ABLATE_RHS
-  // diagnostic build only (never shipped): same loads and stores, trivial arithmetic
-  fxp = FaceT{u.xp, p.xp};
-  fzp = FaceT{u.zp, p.zp};
-  du = ((fxm.prod + u.ym) + (u.yp + fzm.prod)) + (un + gc);
-  dp = ((fxm.dp + p.ym) + (p.yp + fzm.dp)) + (pc + g.xp + g.ym + g.yp + g.zp);
-  return;
-#endif
   const double rho = gc * c.rho_g + (1.0 - gc) * (pc * c.rho_i + (1.0 - pc) * c.rho_w);
   const double cp = gc * c.cp_g + (1.0 - gc) * (pc * c.cp_i + (1.0 - pc) * c.cp_w);
   const double wi = fmax(0.0, 1.0 - c.zeta * gc);
@@ -295,12 +222,6 @@ struct StageArgs {
   double cin;          // coefficient of the stage-input combine: h3, h6, h8, h for stages 2..5
   int gwx, gty;        // merson_fused tile: gwx cell pairs x gty rows (fused_geometry)
   int gl_keep;         // stage 5: x(t+h) of gl is not stored, XN already holds it (pft_slab_set_gl_keep)
-  // ipc transport (merson_fused): the output's boundary planes are also stored into the
-  // neighbours' ghost planes -- plane 0 to plo (the neighbour below's top ghost plane, field 0),
-  // plane n3-1 to phi (the neighbour above's bottom ghost plane); null: no neighbour that side
-  double* plo;
-  double* phi;
-  long plo_fs, phi_fs;
   // stage 5 (merson_fused): the last workgroup to finish publishes the error norm straight to
   // pinned host memory (pub[0] eps bits, pub[1] non-finite flag, both pre-set to a sentinel by
   // the host) and resets the accumulator; pub_count counts the finished workgroups
@@ -515,51 +436,11 @@ __global__ __launch_bounds__(PFT_BLOCK) void merson_stage(StageArgs a, pft_const
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
 // LDS doubles per field and plane of merson_fused: (2 gwx + 4)(gty + 2) <= 680 (64 x 8 tiles)
-#if PFT_FBLOCK > 256
-#define PFT_FUSED_LF 1224
-#else
 #define PFT_FUSED_LF 680
-#endif
 
-template <int WX>
-struct TileGeo {
-  static constexpr int TX = 2 * WX;              // cells in x
-  static constexpr int TY = PFT_BLOCK / WX;      // rows in y
-  static constexpr int LW = TX + 4;              // LDS row: 2-cell halo each side (16-B pairs)
-  static constexpr int LH = TY + 2;              // LDS rows: 1-row halo
-  static constexpr int LF = LW * LH;             // doubles per field and plane
-  static constexpr int NH = LW + 2 * TY;         // halo pairs per field: 2 rows of LW/2, 2 per inner row
-};
-
-#ifndef PFT_NT_STORE
-#define PFT_NT_STORE 0
-#endif
-#ifndef PFT_NT_LOAD
-#define PFT_NT_LOAD 0
-#endif
-__device__ __forceinline__ dbl2 ld2(const double* p)
-{
-#if PFT_NT_LOAD
-  return __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(p));
-#else
-  return *reinterpret_cast<const dbl2*>(p);
-#endif
-}
-__device__ __forceinline__ void st2(double* p, dbl2 v)
-{
-#if PFT_NT_STORE
-  __builtin_nontemporal_store(v, reinterpret_cast<dbl2*>(p));
-#else
-  *reinterpret_cast<dbl2*>(p) = v;
-#endif
-}
-// a boundary plane's output pair also goes to the z-neighbour's ghost plane (ipc transport)
-__device__ __forceinline__ void push2(const StageArgs& a, int k, int q, long po, dbl2 v)
-{
-  if (k == 0 && a.plo) st2(a.plo + q * a.plo_fs + po, v);
-  if (k == a.n3 - 1 && a.phi) st2(a.phi + q * a.phi_fs + po, v);
-}
-
+// (non-temporal loads measured -25%, non-temporal stores +-0: plain accesses)
+__device__ __forceinline__ dbl2 ld2(const double* p) { return *reinterpret_cast<const dbl2*>(p); }
+__device__ __forceinline__ void st2(double* p, dbl2 v) { *reinterpret_cast<dbl2*>(p) = v; }
 // store a pair with its halves exchanged when sw = 1 (two 8-byte stores at per-thread offsets)
 __device__ __forceinline__ void st2x(double* p, dbl2 v, int sw)
 {
@@ -567,179 +448,8 @@ __device__ __forceinline__ void st2x(double* p, dbl2 v, int sw)
   p[1 - sw] = v.y;
 }
 
-template <int STAGE, int MODE, bool GLS, int WX>
-__global__ __launch_bounds__(PFT_BLOCK) void merson_tile(StageArgs a, pft_consts c)
-{
-  using G = TileGeo<WX>;
-  __shared__ __attribute__((aligned(16))) double lds[2][3][G::LF];
-
-  const int ntx = (a.n1 + G::TX - 1) / G::TX;
-  const int lin = xcd_remap(blockIdx.x, a.ntile * a.nchunk);
-  const int tile = lin % a.ntile, chunk = lin / a.ntile;
-  const int x0 = (tile % ntx) * G::TX, y0 = (tile / ntx) * G::TY;
-  const int tx = threadIdx.x % WX, ty = threadIdx.x / WX;
-  const int i0 = x0 + 2 * tx, j = y0 + ty;
-  const bool active = (i0 < a.n1) && (j < a.n2);
-  const long po = (long)(j < a.n2 ? j : a.n2 - 1) * a.n1 + (i0 < a.n1 ? i0 : a.n1 - 2);   // own pair
-  const int kb = a.k_begin + chunk * a.kz;
-  const int ke = min(kb + a.kspan, a.k_end);
-  const int lo = (ty + 1) * G::LW + 2 + 2 * tx;                                            // own pair in LDS
-
-  // halo pair served by this thread (field hf, LDS index hl, plane offset hp)
-  const int t = threadIdx.x;
-  const bool hact = t < 3 * G::NH;
-  const int hf = hact ? t / G::NH : 0, h = hact ? t % G::NH : 0;
-  int hr, hcp;
-  if (h < G::LW / 2) { hr = 0; hcp = h; }
-  else if (h < G::LW) { hr = G::LH - 1; hcp = h - G::LW / 2; }
-  else { const int q = h - G::LW; hr = 1 + q / 2; hcp = (q & 1) ? G::LW / 2 - 1 : 0; }
-  const int hi = x0 - 2 + 2 * hcp, hj = y0 + hr - 1;
-  const bool hin = hi >= 0 && hi < a.n1 && hj >= 0 && hj < a.n2;
-  const long hp = hin ? (long)hj * a.n1 + hi : po;        // out of the domain: never read (walls)
-  const int hl = hr * G::LW + 2 * hcp;
-
-  const double* fin[3] = {a.in, a.in + a.fs, GLS ? a.x + 2 * a.fs : a.in + 2 * a.fs};
-  const double* hsrc = fin[hf] + hp;
-
-  double m = 0.0;
-  bool nf = false;
-  dbl2 zm[3], zc[3], zp[3], zn[3];
-  int cur = 0;
-  if (kb < ke) {
-    const long o0 = (long)(kb + 1) * a.plane + po;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      zc[q] = ld2(fin[q] + o0);
-      zm[q] = (kb == 0 && !a.has_below) ? zc[q] : ld2(fin[q] + o0 - a.plane);
-      zp[q] = (kb == a.n3 - 1 && !a.has_above) ? zc[q] : ld2(fin[q] + o0 + a.plane);
-      st2(&lds[0][q][lo], zc[q]);
-    }
-    if (hact) st2(&lds[0][hf][hl], ld2(hsrc + (long)(kb + 1) * a.plane));
-    __syncthreads();
-  }
-  for (int k = kb; k < ke; ++k) {
-    const long o = (long)(k + 1) * a.plane + po;
-    const bool top = (k == a.n3 - 1) && !a.has_above;
-    const bool more = k + 1 < ke;
-    // pointwise operands of this plane's combine
-    dbl2 xv[3], k1v[3], k3v[3], k4v[3];
-    if (STAGE >= 1) {
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        if (GLS && q == 2) continue;
-        xv[q] = ld2(a.x + q * a.fs + o);
-        if (STAGE >= 2) k1v[q] = ld2(a.k1 + q * a.fs + o);
-        if (STAGE >= 4) k3v[q] = ld2(a.k3 + q * a.fs + o);
-        if (STAGE >= 5) k4v[q] = ld2(a.k4 + q * a.fs + o);
-      }
-    }
-    // stage plane k+1 into the other buffer: own centres now, the halo ring after the arithmetic
-    dbl2 hv = {0.0, 0.0};
-    if (more) {
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        zn[q] = ld2(fin[q] + o + 2 * (long)a.plane);
-        st2(&lds[cur ^ 1][q][lo], zp[q]);
-      }
-      if (hact) hv = ld2(hsrc + (long)(k + 2) * a.plane);
-    }
-    double du[2], dp[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      Col col[3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const double* L = lds[cur][q];
-        const double cen = zc[q][s];
-        col[q].c = cen;
-        if (s == 0) {
-          col[q].xm = i0 > 0 ? L[lo - 1] : cen;
-          col[q].xp = zc[q][1];
-        } else {
-          col[q].xm = zc[q][0];
-          col[q].xp = i0 + 2 < a.n1 ? L[lo + 2] : cen;
-        }
-        col[q].ym = j > 0 ? L[lo - G::LW + s] : cen;
-        col[q].yp = j < a.n2 - 1 ? L[lo + G::LW + s] : cen;
-        col[q].zm = zm[q][s];
-        col[q].zp = top ? cen : zp[q][s];
-      }
-      if (top) col[0].zp = a.T_top;
-      const double un = a.noise ? zc[0][s] + a.noise[(long)k * a.plane + po + s] : zc[0][s];
-      rhs_cell<MODE>(c, col[0], col[1], col[2], un, du[s], dp[s]);
-    }
-    if (more && hact) st2(&lds[cur ^ 1][hf][hl], hv);
-    if (active) {
-      if (STAGE == 0) {
-        st2(a.kout + o, dbl2{du[0], du[1]});
-        st2(a.kout + a.fs + o, dbl2{dp[0], dp[1]});
-        st2(a.kout + 2 * a.fs + o, dbl2{0.0, 0.0});
-      } else {
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-          if (GLS && q == 2) continue;
-          const dbl2 K = q == 0 ? dbl2{du[0], du[1]} : (q == 1 ? dbl2{dp[0], dp[1]} : dbl2{0.0, 0.0});
-          const long e = q * a.fs + o;
-          dbl2 r;
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            if (STAGE == 1) r[s] = K[s] * a.coef + xv[q][s];                                   // hybrid2.c:388
-            else if (STAGE == 2) r[s] = (k1v[q][s] + K[s]) * a.coef + xv[q][s];                 // :408
-            else if (STAGE == 3) r[s] = (k1v[q][s] + 3.0 * K[s]) * a.coef + xv[q][s];           // :428
-            else if (STAGE == 4) r[s] = (0.5 * k1v[q][s] - 1.5 * k3v[q][s] + 2.0 * K[s]) * a.h + xv[q][s];  // :449
-            else {
-              const double em = q == 0 ? a.em0 : (q == 1 ? a.em1 : a.em2);
-              const double ev = em * fabs(0.2 * k1v[q][s] - 0.9 * k3v[q][s] + 0.8 * k4v[q][s] - 0.1 * K[s]);  // :521
-              if (ev > m) m = ev;                                                               // NaN never wins
-              nf |= !isfinite(ev);
-              r[s] = xv[q][s] + a.coef * (0.5 * (k1v[q][s] + K[s]) + 2.0 * k4v[q][s]);          // :667
-            }
-          }
-          if (STAGE == 1 || STAGE == 3 || STAGE == 4) st2(a.kout + e, K);
-          st2(a.out + e, r);
-        }
-      }
-    }
-    __syncthreads();
-    cur ^= 1;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      zm[q] = zc[q];
-      zc[q] = zp[q];
-      zp[q] = zn[q];
-    }
-  }
-
-  if (STAGE == 5) {
-    __shared__ double red[PFT_BLOCK / 64];
-    __shared__ int rnf[PFT_BLOCK / 64];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const double ov = __shfl_xor(m, off, 64);
-      if (ov > m) m = ov;
-    }
-    const int anynf = __any(nf);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-      red[w] = m;
-      rnf[w] = anynf;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double bm = red[0];
-      int bnf = rnf[0];
-      for (int q = 1; q < PFT_BLOCK / 64; ++q) {
-        if (red[q] > bm) bm = red[q];
-        bnf |= rnf[q];
-      }
-      if (bm > 0.0) atomicMax(a.eps_bits, (unsigned long long)__double_as_longlong(bm));
-      if (bnf) atomicOr(a.nonfinite, 1u);
-    }
-  }
-}
-
 // ------------------------------------------------------------------------------------------
-// the recompute kernel (default): like merson_tile, but no stage-input ("aux") array exists.
+// the recompute kernel (default): an LDS tile, and no stage-input ("aux") array exists.
 // The reference writes aux = combine(x, K...) after each stage and the next RHS reads it
 // (hybrid2.c:378-450); here each stage kernel reads x and the K's its input is made of and
 // evaluates the same combine, with the same operands in the same order, while staging the plane
@@ -755,7 +465,6 @@ __device__ __forceinline__ void load_ops(const StageArgs& a, int q, long o, Ops&
 {
   r.x = ld2(a.x + q * a.fs + o);
   if (GLS && q == 2) return;                     // dgl == 0: the gl input is x (F4)
-#if PFT_GLK_LITERAL
   if (q == 2) {
     // gl's K's are the literal 0.0 the model's RHS writes for dgl (equation.c:731,874): never
     // stored, never loaded; the stage combines still run on them (stage_in, stage 5), so the gl
@@ -764,9 +473,8 @@ __device__ __forceinline__ void load_ops(const StageArgs& a, int q, long o, Ops&
     r.k1 = z; r.k2 = z; r.k3 = z; r.k4 = z;
     return;
   }
-#endif
-  if (STAGE >= 2 && !(STAGE == 3 && PFT_K12_SUM)) r.k1 = ld2(a.k1 + q * a.fs + o);
-  if (STAGE == 3) r.k2 = ld2(a.k2 + q * a.fs + o);   // K2, or S = K1 + K2 (PFT_K12_SUM)
+  if (STAGE >= 2 && STAGE != 3) r.k1 = ld2(a.k1 + q * a.fs + o);
+  if (STAGE == 3) r.k2 = ld2(a.k2 + q * a.fs + o);   // S = K1 + K2, stored by stage 2
   if (STAGE >= 4) r.k3 = ld2(a.k3 + q * a.fs + o);
   if (STAGE == 5) r.k4 = ld2(a.k4 + q * a.fs + o);
 }
@@ -779,7 +487,7 @@ __device__ __forceinline__ dbl2 stage_in(const StageArgs& a, int q, const Ops& r
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     if (STAGE == 2) v[s] = r.k1[s] * a.cin + r.x[s];                                      // hybrid2.c:388
-    if (STAGE == 3) v[s] = (PFT_K12_SUM ? r.k2[s] : r.k1[s] + r.k2[s]) * a.cin + r.x[s];  // :408
+    if (STAGE == 3) v[s] = r.k2[s] * a.cin + r.x[s];                                      // :408 (S = K1 + K2)
     if (STAGE == 4) v[s] = (r.k1[s] + 3.0 * r.k3[s]) * a.cin + r.x[s];                    // :428
     if (STAGE == 5) v[s] = (0.5 * r.k1[s] - 1.5 * r.k3[s] + 2.0 * r.k4[s]) * a.cin + r.x[s];  // :449
   }
@@ -790,17 +498,15 @@ template <bool GLS>
 __device__ __forceinline__ void keep5(int q, const Ops& r, dbl2& x, dbl2& k1, dbl2& k4, dbl2& E)
 {
   x = r.x;
-  if ((GLS || PFT_S5_GLZERO) && q == 2) return;
+  if (q == 2) return;
   k1 = r.k1;
   k4 = r.k4;
 #pragma unroll
   for (int s = 0; s < 2; ++s) E[s] = 0.2 * r.k1[s] - 0.9 * r.k3[s] + 0.8 * r.k4[s];   // hybrid2.c:521 prefix
 }
 
-// PUSH (ipc transport): the output's boundary planes also go to the z-neighbours' ghost planes;
-// a separate instantiation, so that the single-slab kernels carry no extra registers
-template <int STAGE, int MODE, bool GLS, bool PUSH = false>
-__global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT_S5_WAVES2 && STAGE == 5) || ((GLS || PFT_DEEP_ALL) && ((PFT_DEEP_MASK >> STAGE) & 1)) ? 2 : PFT_FUSED_WAVES))) void merson_fused(StageArgs a, pft_consts c)
+template <int STAGE, int MODE, bool GLS>
+__global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAGE >= 1 ? 2 : 3))) void merson_fused(StageArgs a, pft_consts c)
 {
   // tile geometry chosen by the host per grid (fused_geometry): gwx pairs x gty rows, so that the
   // tiles fit n1 and n2 without mostly-idle edge workgroups (n1 = 200: 50 x 10 cells)
@@ -848,25 +554,22 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT
   bool nf = false;
   dbl2 zm[3], zc[3], zp[3];
   constexpr bool FLUX = MODE != 10 && MODE != 11;
-  // face reuse (rhs_cell_f) in every stage.  Stage 5 holds two planes of combine operands; only
-  // with gl's K's literal (PFT_S5_FACE) or gl_static does the z-face carry fit beside them (235
-  // VGPRs, no spills; with gl's K's materialised it spilled: 0.505 vs 0.470 ms)
-  constexpr bool FACE = STAGE != 5 || GLS || PFT_S5_FACE;
-  // two-deep z pipeline (stages in PFT_DEEP_MASK; gl_static, and every mode once gl's K's are
-  // literal, PFT_DEEP_ALL): the raw operands of plane k+2 are loaded while plane k is computed (the
-  // stage input of plane k+1 is its z+1 neighbour, so a one-deep pipeline waits for its loads
-  // before the stencil).  It costs the operand registers: 2 waves/SIMD.  Measured at 400^3:
-  // stages 3-4 0.258 vs 0.288-0.296 ms, stage 1 0.158 vs 0.166, stage 2 0.217 vs 0.222.
-  constexpr bool DEEP = (GLS || PFT_DEEP_ALL) && ((PFT_DEEP_MASK >> STAGE) & 1) != 0 && STAGE >= 1 && STAGE <= 4;
+  // face reuse (rhs_cell_f) in every stage; stage 5 holds two planes of combine operands beside
+  // the z-face carry (235 VGPRs, no spills)
+  // two-deep z pipeline (stages 1-4): the raw operands of plane k+2 are loaded while plane k is
+  // computed (the stage input of plane k+1 is its z+1 neighbour, so a one-deep pipeline waits for
+  // its loads before the stencil).  It costs the operand registers: 2 waves/SIMD.  Measured at
+  // 400^3: stages 3-4 0.258 vs 0.288-0.296 ms, stage 1 0.158 vs 0.166, stage 2 0.217 vs 0.222.
+  constexpr bool DEEP = STAGE >= 1 && STAGE <= 4;
   Ops pn[3], ph;                       // DEEP: operands of plane k+1 (centre, halo pair)
   FaceT fz[2];                         // z-face below plane k of each cell of the pair
-  constexpr bool SUM2 = STAGE == 2 && PFT_K12_SUM;
-  constexpr bool SUM2K = SUM2 && !PFT_K12_RELOAD;   // K1 carried in registers
+  // stage 2 stores S = K1 + K2 (stage 3's input combine, hybrid2.c:408), K1 carried in registers
+  // (re-loading it one plane later measured 4% slower)
+  constexpr bool SUM2 = STAGE == 2;
   dbl2 s2c[3], s2n[3];                 // SUM2: K1 of planes k and k+1 (the stored sum's operand)
-#ifdef PFT_S5_KEEP
   // stage 5 keeps x, K1, K4 and the K1/K3/K4 part of the error norm of planes k and k+1
+  // (re-loading them one plane later misses the 4 MiB L2: 0.52 vs 0.65 ms at 400^3)
   dbl2 cx[3], ck1[3], ck4[3], cE[3], nx[3], nk1[3], nk4[3], nE[3];
-#endif
   int cur = 0;
   if (kb < ke) {
     const long o0 = (long)(kb + 1) * a.plane + po;
@@ -875,10 +578,8 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT
       Ops cop;
       load_ops<STAGE, GLS>(a, q, o0, cop);
       zc[q] = stage_in<STAGE, GLS>(a, q, cop);
-      if constexpr (SUM2K) s2c[q] = cop.k1;
-#ifdef PFT_S5_KEEP
+      if constexpr (SUM2) s2c[q] = cop.k1;
       if (STAGE == 5) keep5<GLS>(q, cop, cx[q], ck1[q], ck4[q], cE[q]);
-#endif
       if (kb == 0 && !a.has_below) {
         zm[q] = zc[q];                                  // bottom wall mirror (equation.c:164-174)
       } else {
@@ -902,14 +603,11 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT
       if (hact && kb + 1 < ke) load_ops<STAGE, GLS>(a, hf, (long)(kb + 2) * a.plane + hp, ph);
     }
     // the z-face below the chunk's first plane; later planes inherit it from the plane below
-    if constexpr (FACE) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
-        fz[s] = face_of(c, zm[1][s], zm[2][s], zm[0][s], zc[1][s], zc[2][s], zc[0][s], FLUX);
-    }
+    for (int s = 0; s < 2; ++s)
+      fz[s] = face_of(c, zm[1][s], zm[2][s], zm[0][s], zc[1][s], zc[2][s], zc[0][s], FLUX);
     __syncthreads();
   }
-#pragma unroll PFT_KUNROLL
   for (int k = kb; k < ke; ++k) {
     const long o = (long)(k + 1) * a.plane + po;
     const bool top = (k == a.n3 - 1) && !a.has_above;
@@ -920,15 +618,13 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT
       for (int q = 0; q < 3; ++q) {
         if constexpr (DEEP) {
           zp[q] = stage_in<STAGE, GLS>(a, q, pn[q]);
-          if constexpr (SUM2K) s2n[q] = pn[q].k1;
+          if constexpr (SUM2) s2n[q] = pn[q].k1;
         } else {
           Ops nop;
           load_ops<STAGE, GLS>(a, q, o + a.plane, nop);
           zp[q] = stage_in<STAGE, GLS>(a, q, nop);
-          if constexpr (SUM2K) s2n[q] = nop.k1;
-#ifdef PFT_S5_KEEP
+          if constexpr (SUM2) s2n[q] = nop.k1;
           if (STAGE == 5) keep5<GLS>(q, nop, nx[q], nk1[q], nk4[q], nE[q]);
-#endif
         }
       }
     }
@@ -980,53 +676,39 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT
         col[q].zp = zp[q][s];
       }
       const double un = a.noise ? zc[0][s] + a.noise[(long)k * a.plane + po + s] : zc[0][s];
-      if constexpr (FACE) {
-        const FaceT fxm =
-            s == 0 ? face_of(c, col[1].xm, col[2].xm, col[0].xm, col[1].c, col[2].c, col[0].c, FLUX) : fx;
-        FaceT fzp;
-        rhs_cell_f<MODE>(c, col[0], col[1], col[2], un, fxm, fz[s], fx, fzp, du[s], dp[s]);
-        fz[s] = fzp;
-      } else {
-        rhs_cell<MODE>(c, col[0], col[1], col[2], un, du[s], dp[s]);
-      }
+      const FaceT fxm =
+          s == 0 ? face_of(c, col[1].xm, col[2].xm, col[0].xm, col[1].c, col[2].c, col[0].c, FLUX) : fx;
+      FaceT fzp;
+      rhs_cell_f<MODE>(c, col[0], col[1], col[2], un, fxm, fz[s], fx, fzp, du[s], dp[s]);
+      fz[s] = fzp;
     }
     if (more && hact) st2x(&lds[cur ^ 1][hf][hl], hv, h0);
     if (active) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
-        if (q == 2 && STAGE != 0 && (GLS || (PFT_GLK_LITERAL && STAGE <= 4))) continue;
+        if (q == 2 && STAGE != 0 && (GLS || STAGE <= 4)) continue;   // gl's K's: literal zeros, never stored
         const dbl2 K = q == 0 ? dbl2{du[0], du[1]} : (q == 1 ? dbl2{dp[0], dp[1]} : dbl2{0.0, 0.0});
         const long e = q * a.fs + o;
         if (SUM2) {
           dbl2 S;
-          const dbl2 k1c = SUM2K ? s2c[q] : ((PFT_GLK_LITERAL && q == 2) ? dbl2{0.0, 0.0} : ld2(a.k1 + e));
+          const dbl2 k1c = s2c[q];
 #pragma unroll
           for (int s = 0; s < 2; ++s) S[s] = k1c[s] + K[s];   // K1 + K2, hybrid2.c:408
           st2(a.kout + e, S);
         } else if (STAGE <= 4) {
           st2(a.kout + e, K);
         } else {
-          // operands of plane k again (loaded one iteration ago: an L2 hit; keeping them in
-          // registers as well would double the stage-5 register file and halve occupancy)
-#ifdef PFT_S5_KEEP
-          // gl (q = 2): K1, K4 and the K part of the error norm are the exact zeros the stages
-          // stored for dgl (equation.c:731), so they are not carried in registers
+          // the combine operands of plane k, kept in registers since they were loaded
+          // gl (q = 2): K1, K4 and the K part of the error norm are the literal zeros of dgl
+          // (equation.c:731), so they are not carried in registers
           constexpr dbl2 zero2 = {0.0, 0.0};
-          const bool z2 = PFT_S5_GLZERO && q == 2;
+          const bool z2 = q == 2;
           const dbl2 ox = cx[q], ok1 = z2 ? zero2 : ck1[q], ok4 = z2 ? zero2 : ck4[q];
           dbl2 oE = cE[q];
           if (z2) {
 #pragma unroll
             for (int s = 0; s < 2; ++s) oE[s] = 0.2 * 0.0 - 0.9 * 0.0 + 0.8 * 0.0;   // :521 prefix
           }
-#else
-          Ops op;
-          load_ops<STAGE, GLS>(a, q, o, op);
-          const dbl2 ox = op.x, ok1 = op.k1, ok4 = op.k4;
-          dbl2 oE;
-#pragma unroll
-          for (int s = 0; s < 2; ++s) oE[s] = 0.2 * op.k1[s] - 0.9 * op.k3[s] + 0.8 * op.k4[s];
-#endif
           dbl2 r;
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
@@ -1046,24 +728,8 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT
     for (int q = 0; q < 3; ++q) {
       zm[q] = zc[q];
       zc[q] = zp[q];
-      if constexpr (SUM2K) s2c[q] = s2n[q];
-#ifdef PFT_S5_KEEP
+      if constexpr (SUM2) s2c[q] = s2n[q];
       if (STAGE == 5) { cx[q] = nx[q]; ck1[q] = nk1[q]; ck4[q] = nk4[q]; cE[q] = nE[q]; }
-#endif
-    }
-  }
-
-  if constexpr (PUSH) {
-    // the output's boundary planes, stored by this very thread in the march above, also go to the
-    // z-neighbours' ghost planes: read back (own stores, L2-hot) and stored once the march is
-    // over, so the march itself holds no extra registers.  The fields are the ones stored.
-    if (active && kb < ke) {
-      const double* dst = STAGE == 5 ? a.out : a.kout;
-      const int nq = (GLS || (STAGE <= 4 && PFT_GLK_LITERAL) || (STAGE == 5 && a.gl_keep)) ? 2 : 3;
-      for (int q = 0; q < nq; ++q) {
-        if (kb == 0 && a.plo) push2(a, 0, q, po, ld2(dst + q * a.fs + a.plane + po));
-        if (ke == a.n3 && a.phi) push2(a, a.n3 - 1, q, po, ld2(dst + q * a.fs + (long)a.n3 * a.plane + po));
-      }
     }
   }
 
@@ -1133,39 +799,15 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu((PFT
 // acting pair's own thread does -- so the mirrored stage-B input is the reference's bit for bit.
 // z neighbours of both levels are read from the plane rings (own pair: written by the thread
 // itself; x/y neighbours: written one iteration earlier, behind the barrier).
-#ifndef PFT_PBLOCK
 #define PFT_PBLOCK 512
-#endif
 #define PFT_PAIR_PAD 4          // doubles before / after each LDS field plane: the discarded outer
                                 // cell of a ring pair reads one slot beyond its row
-#ifndef PFT_PAIR_LFA
-#define PFT_PAIR_LFA 1024       // (tx + 4)(ty + 4) + 2 pad doubles per field and plane (stage A input)
-#endif
-#ifndef PFT_PAIR_LFB
-#define PFT_PAIR_LFB 936        // (tx + 4)(ty + 2) + 2 pad (stage B input)
-#endif
+#define PFT_PAIR_LP 44          // LDS row pitch (doubles): tx + 4 <= 44, a compile-time constant so
+                                // that every LDS access is a per-lane base + an immediate offset
+#define PFT_PAIR_LFA 1024       // 44 (ty + 4) + 2 pad doubles per field and plane (stage A input)
+#define PFT_PAIR_LFB 936        // 44 (ty + 2) + 2 pad (stage B input)
 #ifndef PFT_PAIR_MIN_CELLS_PER_CU
 #define PFT_PAIR_MIN_CELLS_PER_CU 16384
-#endif
-// pairs (bit SA) whose stage-B input operands stay in registers instead of being re-loaded
-#ifndef PFT_PAIR_RES_MASK
-#define PFT_PAIR_RES_MASK ((1 << 2) | (1 << 4))
-#endif
-#ifndef PFT_PAIR_SCHED
-#define PFT_PAIR_SCHED 0
-#endif
-// wave priorities in the pair kernels' z-loop (merson_pair, PRIO): pair 2+3, pair 4+5
-#ifndef PFT_PAIR_PRIO2
-#define PFT_PAIR_PRIO2 1
-#endif
-#ifndef PFT_PAIR_PRIO4
-#define PFT_PAIR_PRIO4 2
-#endif
-#ifndef PFT_PAIR_LATE_LA_MASK
-#define PFT_PAIR_LATE_LA_MASK 0
-#endif
-#ifndef PFT_PAIR_LATE_MASK
-#define PFT_PAIR_LATE_MASK (1 << 4)
 #endif
 
 struct PairArgs {
@@ -1188,7 +830,13 @@ struct PairArgs {
   double T_topA, T_topB;   // Dirichlet u above the top plane at the two stage times
   double cinA, cinB;    // stage-input coefficients: h/3, h/6 (2+3); h/8, h (4+5)
   double coef;          // x(t+h) coefficient h/3 (4+5)
-  double em0, em1, em2;
+  double em0, em1;
+  // gl's K's are the literal zeros of dgl (equation.c:731,874), so every gl term of the step is a
+  // per-launch constant the host evaluates with the reference's expression (pair_gl_consts):
+  // stage A's and stage B's gl input are glA + x and glB + x, x(t+h) of gl is x + glX, and gl's
+  // error-norm term is evgl.  GLX kernels (gl_static, or gl_keep: x's gl holds no -0.0 or NaN and
+  // the coefficients are finite) read gl's inputs straight from x: glA + x == x bit for bit there.
+  double glA, glB, glX, evgl;
   int gl_keep;
 };
 // byte offset of the kernel's second argument (pft_consts) in the kernarg segment
@@ -1199,31 +847,15 @@ static constexpr unsigned PFT_PAIR_COFF =
 // scalar loads at each of its three phases (PFT_PAIR_BIND: the pointer is laundered through an
 // empty asm, so the loads cannot be hoisted out of the loop).  Kept live across the whole loop,
 // the ~25 model constants, the array bases and the step coefficients needed ~190 SGPRs: ~90 were
-// spilled into VGPR lanes and re-read by ~160 v_readlane per iteration.
-// Pairs (bit SA) that do so: both -- pair 4+5 0.519 -> 0.486 ms at 400^3; pair 2+3 (~15 SGPRs
-// spilled) 0.408 -> 0.403 ms once the wave priorities below were in (2% slower before them).
-#ifndef PFT_PAIR_KREL_MASK
-#define PFT_PAIR_KREL_MASK ((1 << 2) | (1 << 4))
-#endif
+// spilled into VGPR lanes and re-read by ~160 v_readlane per iteration (pair 4+5 0.519 -> 0.486 ms
+// at 400^3; pair 2+3 0.408 -> 0.403 ms).
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef const __attribute__((address_space(4))) char* pft_kptr;
-template <bool K>
-__device__ __forceinline__ const PairArgs& pair_bind_a(const PairArgs& a, pft_kptr q)
-{
-  if constexpr (K) return *(const __attribute__((address_space(4))) PairArgs*)q;
-  else return a;
-}
-template <bool K>
-__device__ __forceinline__ const pft_consts& pair_bind_c(const pft_consts& c, pft_kptr q)
-{
-  if constexpr (K) return *(const __attribute__((address_space(4))) pft_consts*)(q + PFT_PAIR_COFF);
-  else return c;
-}
-#define PFT_PAIR_BIND(A, C)                                \
-  pft_kptr kq_##A = kbase;                                \
-  if (KREL) asm volatile("" : "+s"(kq_##A));              \
-  const PairArgs& A = pair_bind_a<KREL>(a, kq_##A);       \
-  const pft_consts& C = pair_bind_c<KREL>(c, kq_##A)
+#define PFT_PAIR_BIND(A, C)                                                                  \
+  pft_kptr kq_##A = kbase;                                                                  \
+  asm volatile("" : "+s"(kq_##A));                                                          \
+  const PairArgs& A = *(const __attribute__((address_space(4))) PairArgs*)kq_##A;           \
+  const pft_consts& C = *(const __attribute__((address_space(4))) pft_consts*)(kq_##A + PFT_PAIR_COFF)
 #else
 #define PFT_PAIR_BIND(A, C) \
   const PairArgs& A = a;    \
@@ -1251,12 +883,12 @@ __device__ __forceinline__ void stb(double* base, unsigned bo, dbl2 v)
 // operands of plane m in [-2, n3 + 1] (interior 0..n3-1; -1 and n3 the ghost planes, -2 and n3+1
 // the far ghost planes of the two-plane halo) at byte offset bo = pbo(m).  The PairArgs pointers
 // are the buffers' pointers minus one plane (run_pair): field q holds plane m at q fs + (m + 2)
-// plane from there, so every offset is unsigned.
-template <int SA>
+// plane from there, so every offset is unsigned.  gl's x is loaded only where an input needs it.
+template <int SA, bool GL = true>
 __device__ __forceinline__ void pair_load(const PairArgs& a, unsigned bo, PairRaw& r)
 {
 #pragma unroll
-  for (int q = 0; q < 3; ++q) r.x[q] = ldb(a.x + q * a.fs, bo);
+  for (int q = 0; q < (GL ? 3 : 2); ++q) r.x[q] = ldb(a.x + q * a.fs, bo);
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
     r.k1[q] = ldb(a.k1 + q * a.fs, bo);
@@ -1264,14 +896,17 @@ __device__ __forceinline__ void pair_load(const PairArgs& a, unsigned bo, PairRa
   }
 }
 
-// stage A's input (stage 2: hybrid2.c:388; stage 4: :428) -- the expressions of stage_in
-template <int SA, bool GLS>
+// stage A's input (stage 2: hybrid2.c:388; stage 4: :428) -- the expressions of stage_in; gl:
+// glA + x (the combine of its literal-zero K's, a per-launch constant), x itself under GLX
+template <int SA, bool GLX>
 __device__ __forceinline__ dbl2 pair_in_A(const PairArgs& a, int q, const PairRaw& r)
 {
-  if (GLS && q == 2) return r.x[2];
-  constexpr dbl2 z = {0.0, 0.0};
-  const dbl2 k1 = q < 2 ? r.k1[q < 2 ? q : 0] : z;
-  const dbl2 k3 = (SA == 4 && q < 2) ? r.k3[q < 2 ? q : 0] : z;
+  if (q == 2) {
+    if (GLX) return r.x[2];
+    return dbl2{a.glA + r.x[2][0], a.glA + r.x[2][1]};
+  }
+  const dbl2 k1 = r.k1[q < 2 ? q : 0];
+  const dbl2 k3 = r.k3[q < 2 ? q : 0];
   dbl2 v;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -1283,13 +918,15 @@ __device__ __forceinline__ dbl2 pair_in_A(const PairArgs& a, int q, const PairRa
 
 // stage B's input from the operands and stage A's K at the cell (stage 3: (K1 + K2) h/6 + x,
 // hybrid2.c:408; stage 5: (0.5 K1 - 1.5 K3 + 2 K4) h + x, :449)
-template <int SA, bool GLS>
+template <int SA, bool GLX>
 __device__ __forceinline__ dbl2 pair_in_B(const PairArgs& a, int q, const PairRaw& r, dbl2 KA)
 {
-  if (GLS && q == 2) return r.x[2];
-  constexpr dbl2 z = {0.0, 0.0};
-  const dbl2 k1 = q < 2 ? r.k1[q < 2 ? q : 0] : z;
-  const dbl2 k3 = (SA == 4 && q < 2) ? r.k3[q < 2 ? q : 0] : z;
+  if (q == 2) {
+    if (GLX) return r.x[2];
+    return dbl2{a.glB + r.x[2][0], a.glB + r.x[2][1]};
+  }
+  const dbl2 k1 = r.k1[q < 2 ? q : 0];
+  const dbl2 k3 = r.k3[q < 2 ? q : 0];
   dbl2 v;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -1309,14 +946,16 @@ __device__ __forceinline__ dbl2 ld2x(const double* p, int sw)
 }
 
 // the RHS of one cell pair (du, dp of both cells): centre zc, z neighbours zm / zp, x/y
-// neighbours from the LDS plane L at slot lo; the x-face between the pair's cells is evaluated
-// once and the z-face below is carried in fz (rhs_cell_f, bit-exact), as in merson_fused
+// neighbours from the LDS field planes L[q] at slot lo (row pitch PFT_PAIR_LP); the x-face
+// between the pair's cells is evaluated once and the z-face below is carried in fz
+// (rhs_cell_f, bit-exact), as in merson_fused
 template <int MODE>
 __device__ __forceinline__ void pair_rhs(const pft_consts& c, const double* L0, const double* L1, const double* L2,
-                                         int lo, int LW, const dbl2* zm, const dbl2* zc, const dbl2* zp,
+                                         int lo, const dbl2* zm, const dbl2* zc, const dbl2* zp,
                                          const double* nz, FaceT* fz, double* du, double* dp)
 {
   constexpr bool FLUX = MODE != 10 && MODE != 11;
+  constexpr int LW = PFT_PAIR_LP;
   const double* L[3] = {L0, L1, L2};
   FaceT fx;
 #pragma unroll
@@ -1339,28 +978,26 @@ __device__ __forceinline__ void pair_rhs(const pft_consts& c, const double* L0, 
     FaceT fzp;
     rhs_cell_f<MODE>(c, col[0], col[1], col[2], un, fxm, fz[s], fx, fzp, du[s], dp[s]);
     fz[s] = fzp;
-#if PFT_PAIR_SCHED
-    // one cell's stencil at a time: the scheduler would interleave the two cells' loads and
-    // temporaries and run out of registers
-    if (s == 0) __builtin_amdgcn_sched_barrier(0);
-#endif
   }
 }
 
-template <int SA, int MODE, bool GLS>
+template <int N>
+using pft_ic = std::integral_constant<int, N>;
+
+template <int SA, int MODE, bool GLX>
 __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2))) void merson_pair(PairArgs a,
                                                                                                    pft_consts c)
 {
   constexpr bool FLUX = MODE != 10 && MODE != 11;
   constexpr dbl2 zero2 = {0.0, 0.0};
-  constexpr bool KREL = ((PFT_PAIR_KREL_MASK >> SA) & 1) != 0;
+  constexpr int LW = PFT_PAIR_LP;
 #if defined(__HIP_DEVICE_COMPILE__)
   const pft_kptr kbase = (pft_kptr)__builtin_amdgcn_kernarg_segment_ptr();
 #endif
   __shared__ __attribute__((aligned(16))) double lA[3][3][PFT_PAIR_LFA];
   __shared__ __attribute__((aligned(16))) double lB[3][3][PFT_PAIR_LFB];
 
-  const int TX = a.tx, TY = a.ty, LW = TX + 4, WP2 = TX / 2 + 2, NPOS = WP2 * (TY + 4);
+  const int TX = a.tx, TY = a.ty, WP2 = TX / 2 + 2, NPOS = WP2 * (TY + 4);
   const int lin = xcd_remap(blockIdx.x, a.ntile * a.nchunk);
   const int tile = lin % a.ntile, chunk = lin / a.ntile;
   const int x0 = (tile % a.ntx) * TX, y0 = (tile / a.ntx) * TY;
@@ -1373,10 +1010,8 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   const int aj = pj < 0 ? 0 : (pj >= a.n2 ? a.n2 - 1 : pj);
   const int xsw = (pi < 0 || pi >= a.n1) ? 1 : 0;
   const unsigned apo = (unsigned)(aj * a.n1 + ai);
-  // byte offset of the acting pair in (interior) plane m of a field
   // byte offset of the acting pair in plane m of a field, from the PairArgs pointers
   auto pbo = [&](int m) -> unsigned { return ((unsigned)(m + 2) * (unsigned)a.plane + apo) * 8u; };
-  auto slot = [](int p) { return (p + 3) % 3; };             // plane ring slot (p >= -3)
   const int posA = PFT_PAIR_PAD + py * LW + 2 * px;            // this position in lA
   const int posB = PFT_PAIR_PAD + (py - 1) * LW + 2 * px;      // ... in lB (rows 1..ty+2)
   const int actA = PFT_PAIR_PAD + (aj - y0 + 2) * LW + (ai - x0 + 2);   // the acting pair in lA
@@ -1397,164 +1032,179 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
 
   double m = 0.0;
   bool nf = false;
-  // Operands in registers: those of plane mm + 1 (landed: stage A's input) and mm + 2 (in
-  // flight).  Stage B's input needs plane mm's again: kept (RES, pair 2+3) or re-loaded (pair 4+5,
-  // one plane after its first load: an L2 hit, not HBM traffic); stage B's outputs (4+5) need plane
-  // mm - 1's: re-loaded -- keeping all would hold ~60 doubles per thread and spill.  The re-loads
-  // are issued before the look-ahead load of plane mm + 2, so that waiting for them (vmcnt counts
-  // in order) never waits for the HBM look-ahead.
-  constexpr bool RES = ((PFT_PAIR_RES_MASK >> SA) & 1) != 0;
-  // LATE: the output re-load and the look-ahead are issued after stage A (fewer registers live
-  // during stage A; the look-ahead then has stage B and the barrier to land)
-  constexpr bool LATE = ((PFT_PAIR_LATE_MASK >> SA) & 1) != 0;
-  // LATE_LA: the look-ahead load after stage A as well (else at the top: it then has a whole
-  // iteration to land, and waiting for the output re-load at the end of stage B drains it)
-  constexpr bool LATE_LA = ((PFT_PAIR_LATE_LA_MASK >> SA) & 1) != 0;
-  constexpr int PRIO = SA == 2 ? PFT_PAIR_PRIO2 : PFT_PAIR_PRIO4;
-  PairRaw rn, rnn, rcr;
-  dbl2 kao[2] = {zero2, zero2};  // stage A's K (u, p) at plane mm - 1
+  // Operands in registers: those of plane mm (stage B's input), mm + 1 (landed: stage A's input)
+  // and mm + 2 (in flight), rotating through R[0..2]; stage B's outputs (4+5) need plane mm - 1's
+  // again: re-loaded after stage A (keeping them would hold ~60 doubles per thread and spill).
+  // Plane p's LDS ring slot is (p - mA0) mod 3 and the loop is unrolled three times, so every ring
+  // slot -- and with the fixed row pitch every LDS offset -- is a compile-time constant, and the
+  // register rotation needs no copies.
+  PairRaw R[3];
+  dbl2 KA[3][2];        // stage A's K (u, p) of the last three planes, rotating with R
   FaceT fzA[2], fzB[2];
 
-  // prologue: stage A's input of planes mA0 - 1 (if any) and mA0 into the ring; operands of mA0
-  // kept, of mA0 + 1 in flight.  (kb >= ke: an empty chunk, which still takes part in the error
-  // norm's workgroup count below)
+  // prologue: stage A's input of planes mA0 - 1 (if any) and mA0 into the ring (slots 2 and 0);
+  // operands of mA0 kept, of mA0 + 1 in flight.  (kb >= ke: an empty chunk, which still takes
+  // part in the error norm's workgroup count below)
   if (kb < ke) {
     dbl2 ia0[3], iam[3];
-    PairRaw rc;
-    pair_load<SA>(a, pbo(mA0), rc);
+    pair_load<SA>(a, pbo(mA0), R[0]);
     if (mA0 > mfirst) {
       PairRaw t;
       pair_load<SA>(a, pbo(mA0 - 1), t);
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
-        iam[q] = pair_in_A<SA, GLS>(a, q, t);
-        st2x(&lA[slot(mA0 - 1)][q][posA], iam[q], xsw);
+        iam[q] = pair_in_A<SA, GLX>(a, q, t);
+        st2x(&lA[2][q][posA], iam[q], xsw);
       }
     }
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      ia0[q] = pair_in_A<SA, GLS>(a, q, rc);
-      st2x(&lA[slot(mA0)][q][posA], ia0[q], xsw);
-      if (mA0 == mfirst) iam[q] = ia0[q];                    // bottom wall: mirror (equation.c:164-174)
+      ia0[q] = pair_in_A<SA, GLX>(a, q, R[0]);
+      st2x(&lA[0][q][posA], ia0[q], xsw);
+      if (mA0 == mfirst) {
+        // bottom wall: plane -1 mirrors plane 0 (equation.c:164-174), also in the ring slot of
+        // plane -1, so that the z-loop reads its z neighbours without selects
+        iam[q] = ia0[q];
+        st2x(&lA[2][q][posA], ia0[q], xsw);
+      }
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) fzA[s] = face_of(c, iam[1][s], iam[2][s], iam[0][s], ia0[1][s], ia0[2][s], ia0[0][s], FLUX);
-    if (mA0 + 1 <= mlast) pair_load<SA>(a, pbo(mA0 + 1), rn);
-    if (RES) rcr = rc;
+    if (mA0 + 1 <= mlast) pair_load<SA>(a, pbo(mA0 + 1), R[1]);
+    KA[2][0] = KA[2][1] = zero2;
     __syncthreads();
   }
 
-  for (int mm = mA0; kb < ke && mm <= ke; ++mm) {
-    const int sA = slot(mm), sAm = slot(mm - 1), sAp = slot(mm + 1);   // ring slots of planes mm, mm-1, mm+1
-    PFT_PAIR_BIND(A0, C0);
-    // stage A's input of plane mm + 1 (own pair: read back by this thread in this iteration; x/y
-    // neighbours: in the next one, behind the barrier)
-    if (mm + 1 <= mlast) {
+  // one z-step: stage A at plane mm, stage B at plane mm - 1; false after the chunk's last one
+  auto step = [&](auto ph, int mm, PairRaw& rc, PairRaw& rn, PairRaw& rnn) -> bool {
+    constexpr int PH = decltype(ph)::value;
+    constexpr int sA = PH, sAm = (PH + 2) % 3, sAp = (PH + 1) % 3;   // ring slots of planes mm, mm-1, mm+1
+    {
+      PFT_PAIR_BIND(A0, C0);
+      (void)C0;
+      // stage A's input of plane mm + 1 (own pair: read back by this thread in this iteration;
+      // x/y neighbours: in the next one, behind the barrier)
+      if (mm + 1 <= mlast) {
 #pragma unroll
-      for (int q = 0; q < 3; ++q) st2x(&lA[sAp][q][posA], pair_in_A<SA, GLS>(A0, q, rn), xsw);
+        for (int q = 0; q < 3; ++q) st2x(&lA[sAp][q][posA], pair_in_A<SA, GLX>(A0, q, rn), xsw);
+      }
+      if (mm + 2 <= mlast) pair_load<SA>(A0, pbo(mm + 2), rnn);          // look-ahead
     }
     const int kB = mm - 1;                                   // stage B's plane
-    PairRaw rc, ro;
-    if (!RES && mm <= mA1 && isA) pair_load<SA>(A0, pbo(mm), rc);   // plane mm again
-    if (RES) rc = rcr;
-    if (!LATE && SA == 4 && kB >= kb && isB) pair_load<SA>(A0, pbo(mm - 1), ro);   // plane kB (outputs)
-    if (!LATE_LA && mm + 2 <= mlast) pair_load<SA>(A0, pbo(mm + 2), rnn);          // look-ahead
-
-    PFT_PAIR_BIND(A1, C1);
-    // The two waves of a SIMD (w and w + 4) run the same phase between two barriers, so their
-    // stalls coincide.  PRIO: waves 0-3 get issue precedence in stage A (1: waves 4-7 in stage B,
-    // 2: nobody in stage B), so the two drift apart and fill each other's stalls.  Measured (A/B,
-    // one box): pair 4+5 0.496 -> 0.483 ms (1) / 0.480 ms (2); pair 2+3 0.407 -> 0.406 (1) /
-    // 0.415 (2); precedence by wave parity instead of halves: slower (0.505).
-    if (PRIO) {
+    PairRaw ro;
+    {
+      PFT_PAIR_BIND(A1, C1);
+      // The two waves of a SIMD (w and w + 4) run the same phase between two barriers, so their
+      // stalls coincide.  Waves 0-3 get issue precedence in stage A (pair 2+3: waves 4-7 in stage
+      // B, pair 4+5: nobody), so the two drift apart and fill each other's stalls.  Measured (A/B,
+      // one box): pair 4+5 0.496 -> 0.480 ms; pair 2+3 0.425 -> 0.403 ms.
       if ((threadIdx.x >> 8) == 0) __builtin_amdgcn_s_setprio(2);
       else __builtin_amdgcn_s_setprio(0);
-    }
-    dbl2 ka[2] = {zero2, zero2};
-    if (mm <= mA1 && isA) {
-      // stage A at plane mm, evaluated as the acting pair's thread does
-      dbl2 zc[3], zm[3], zp[3];
+      dbl2 (&ka)[2] = KA[PH];
+      ka[0] = ka[1] = zero2;
+      if (mm <= mA1 && isA) {
+        // stage A at plane mm, evaluated as the acting pair's thread does
+        if (mm == n3 - 1 && whi) {
+          // top wall: the ring slot of plane n3 holds the ghost values -- Dirichlet u (equation.c:
+          // 175-183), p and gl mirrored -- at this position (its own z neighbour only)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        zc[q] = ld2x(&lA[sA][q][posA], xsw);
-        zm[q] = (mm > 0 || !wlo) ? ld2x(&lA[sAm][q][posA], xsw) : zc[q];
-        zp[q] = (mm < n3 - 1 || !whi) ? ld2x(&lA[sAp][q][posA], xsw) : zc[q];
-      }
-      if (mm == n3 - 1 && whi) zp[0] = dbl2{A1.T_topA, A1.T_topA};     // top: Dirichlet u (equation.c:175-183)
-      double du[2], dp[2];
-      const double* nz = A1.noise ? A1.noise + (long)mm * A1.plane + (long)apo : nullptr;
-      pair_rhs<MODE>(C1, &lA[sA][0][0], &lA[sA][1][0], &lA[sA][2][0], actA, LW, zm, zc, zp, nz, fzA, du, dp);
-      ka[0] = dbl2{du[0], du[1]};
-      ka[1] = dbl2{dp[0], dp[1]};
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        st2x(&lB[sA][q][posB], pair_in_B<SA, GLS>(A1, q, rc, q < 2 ? ka[q < 2 ? q : 0] : zero2), xsw);
-    }
-
-    PFT_PAIR_BIND(A2, C2);
-    if (PRIO == 2) {
-      __builtin_amdgcn_s_setprio(0);
-    } else if (PRIO == 1) {
-      if ((threadIdx.x >> 8) == 0) __builtin_amdgcn_s_setprio(0);
-      else __builtin_amdgcn_s_setprio(2);
-    }
-    // (a build that skips this re-load -- wrong results, timing only -- ran 1% faster: the
-    // re-load's latency hides behind stage B's stencil)
-    if (LATE && SA == 4 && kB >= kb && isB) pair_load<SA>(A2, pbo(mm - 1), ro);
-    if (LATE_LA && mm + 2 <= mlast) pair_load<SA>(A2, pbo(mm + 2), rnn);
-    if (kB >= kb && isB) {
-      const int sB = slot(kB), sBm = slot(kB - 1), sBp = slot(mm);
-      const int lo = posB;
-      dbl2 zc[3], zm[3], zp[3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        zc[q] = ld2(&lB[sB][q][lo]);
-        zm[q] = (kB > 0 || !wlo) ? ld2(&lB[sBm][q][lo]) : zc[q];
-        zp[q] = (kB < n3 - 1 || !whi) ? ld2(&lB[sBp][q][lo]) : zc[q];
-      }
-      if (kB == n3 - 1 && whi) zp[0] = dbl2{A2.T_topB, A2.T_topB};
-      if (kB == kb) {
-        // the z-face below the chunk's first stage-B plane
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-          fzB[s] = face_of(C2, zm[1][s], zm[2][s], zm[0][s], zc[1][s], zc[2][s], zc[0][s], FLUX);
-      }
-      double du[2], dp[2];
-      const unsigned e0 = pbo(kB);
-      const double* nz = A2.noise ? A2.noise + (long)kB * A2.plane + (long)apo : nullptr;
-      pair_rhs<MODE>(C2, &lB[sB][0][0], &lB[sB][1][0], &lB[sB][2][0], lo, LW, zm, zc, zp, nz, fzB, du, dp);
-      if (SA == 2) {
-        stb(A2.out, e0, dbl2{du[0], du[1]});                   // K3 (hybrid2.c:412-429)
-        stb(A2.out + A2.fs, e0, dbl2{dp[0], dp[1]});
-      } else {
+          for (int q = 1; q < 3; ++q) {
+            lA[sAp][q][posA] = lA[sA][q][posA];
+            lA[sAp][q][posA + 1] = lA[sA][q][posA + 1];
+          }
+          lA[sAp][0][posA] = lA[sAp][0][posA + 1] = A1.T_topA;
+        }
+        dbl2 zc[3], zm[3], zp[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          if (GLS && q == 2) continue;
-          const dbl2 K = q == 0 ? dbl2{du[0], du[1]} : (q == 1 ? dbl2{dp[0], dp[1]} : zero2);
-          const dbl2 k1 = q < 2 ? ro.k1[q < 2 ? q : 0] : zero2;
-          const dbl2 k3 = q < 2 ? ro.k3[q < 2 ? q : 0] : zero2;
-          const dbl2 k4 = q < 2 ? kao[q < 2 ? q : 0] : zero2;
-          dbl2 r;
+          zc[q] = ld2x(&lA[sA][q][posA], xsw);
+          zm[q] = ld2x(&lA[sAm][q][posA], xsw);
+          zp[q] = ld2x(&lA[sAp][q][posA], xsw);
+        }
+        double du[2], dp[2];
+        const double* nz = A1.noise ? A1.noise + (long)mm * A1.plane + (long)apo : nullptr;
+        pair_rhs<MODE>(C1, &lA[sA][0][0], &lA[sA][1][0], &lA[sA][2][0], actA, zm, zc, zp, nz, fzA, du, dp);
+        ka[0] = dbl2{du[0], du[1]};
+        ka[1] = dbl2{dp[0], dp[1]};
 #pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const double em = q == 0 ? A2.em0 : (q == 1 ? A2.em1 : A2.em2);
-            const double ev = em * fabs(0.2 * k1[s] - 0.9 * k3[s] + 0.8 * k4[s] - 0.1 * K[s]);   // :521
-            if (ev > m) m = ev;                                                            // NaN never wins
-            nf |= !isfinite(ev);
-            r[s] = ro.x[q][s] + A2.coef * (0.5 * (k1[s] + K[s]) + 2.0 * k4[s]);            // :667
-          }
-          if (!(q == 2 && A2.gl_keep)) stb(A2.out + q * A2.fs, e0, r);
+        for (int q = 0; q < 3; ++q) {
+          const dbl2 ib = pair_in_B<SA, GLX>(A1, q, rc, q < 2 ? ka[q < 2 ? q : 0] : zero2);
+          st2x(&lB[sA][q][posB], ib, xsw);
+          if (mm == 0 && wlo) st2x(&lB[sAm][q][posB], ib, xsw);   // bottom wall: plane -1 mirrors plane 0
         }
       }
     }
-    if (mm == ke) break;
-    __syncthreads();
-    if (SA == 4) {
-      kao[0] = ka[0];
-      kao[1] = ka[1];
+    {
+      PFT_PAIR_BIND(A2, C2);
+      if (SA == 4) __builtin_amdgcn_s_setprio(0);
+      else if ((threadIdx.x >> 8) == 0) __builtin_amdgcn_s_setprio(0);
+      else __builtin_amdgcn_s_setprio(2);
+      // operands of plane kB for stage B's outputs (4+5), after stage A: fewer registers live
+      // during stage A, and the latency hides behind stage B's stencil
+      // (GLX: gl's x(t+h) is not stored, XN holds it: gl's x is not needed)
+      if (SA == 4 && kB >= kb && isB) pair_load<SA, !GLX>(A2, pbo(kB), ro);
+      if (kB >= kb && isB) {
+        constexpr int sB = (PH + 2) % 3, sBm = (PH + 1) % 3, sBp = PH;   // slots of planes kB, kB-1, kB+1
+        const int lo = posB;
+        if (kB == n3 - 1 && whi) {
+          // top wall: the ghost values of plane n3 at this position (as in stage A above)
+#pragma unroll
+          for (int q = 1; q < 3; ++q) st2(&lB[sBp][q][lo], ld2(&lB[sB][q][lo]));
+          st2(&lB[sBp][0][lo], dbl2{A2.T_topB, A2.T_topB});
+        }
+        dbl2 zc[3], zm[3], zp[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          zc[q] = ld2(&lB[sB][q][lo]);
+          zm[q] = ld2(&lB[sBm][q][lo]);
+          zp[q] = ld2(&lB[sBp][q][lo]);
+        }
+        if (kB == kb) {
+          // the z-face below the chunk's first stage-B plane
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            fzB[s] = face_of(C2, zm[1][s], zm[2][s], zm[0][s], zc[1][s], zc[2][s], zc[0][s], FLUX);
+        }
+        double du[2], dp[2];
+        const unsigned e0 = pbo(kB);
+        const double* nz = A2.noise ? A2.noise + (long)kB * A2.plane + (long)apo : nullptr;
+        pair_rhs<MODE>(C2, &lB[sB][0][0], &lB[sB][1][0], &lB[sB][2][0], lo, zm, zc, zp, nz, fzB, du, dp);
+        if (SA == 2) {
+          stb(A2.out, e0, dbl2{du[0], du[1]});                   // K3 (hybrid2.c:412-429)
+          stb(A2.out + A2.fs, e0, dbl2{dp[0], dp[1]});
+        } else {
+          const dbl2(&kao)[2] = KA[(PH + 2) % 3];              // stage A's K (K4) at plane kB
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const dbl2 K = q == 0 ? dbl2{du[0], du[1]} : dbl2{dp[0], dp[1]};
+            const dbl2 k1 = ro.k1[q], k3 = ro.k3[q], k4 = kao[q];
+            const double em = q == 0 ? A2.em0 : A2.em1;
+            dbl2 r;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              const double ev = em * fabs(0.2 * k1[s] - 0.9 * k3[s] + 0.8 * k4[s] - 0.1 * K[s]);   // :521
+              if (ev > m) m = ev;                                                            // NaN never wins
+              nf |= !isfinite(ev);
+              r[s] = ro.x[q][s] + A2.coef * (0.5 * (k1[s] + K[s]) + 2.0 * k4[s]);            // :667
+            }
+            stb(A2.out + q * A2.fs, e0, r);
+          }
+          // gl: x(t+h) = x + coef (0.5 (0.0 + 0.0) + 2.0 0.0), stored unless XN already holds it
+          if (!GLX && !A2.gl_keep) stb(A2.out + 2 * A2.fs, e0, dbl2{ro.x[2][0] + A2.glX, ro.x[2][1] + A2.glX});
+        }
+      }
     }
-    if (RES) rcr = rn;
-    rn = rnn;
+    if (mm == ke) return false;
+    __syncthreads();
+    return true;
+  };
+
+  if (kb < ke) {
+    for (int mm = mA0;; mm += 3) {
+      if (!step(pft_ic<0>{}, mm, R[0], R[1], R[2])) break;
+      if (!step(pft_ic<1>{}, mm + 1, R[1], R[2], R[0])) break;
+      if (!step(pft_ic<2>{}, mm + 2, R[2], R[0], R[1])) break;
+    }
   }
 
   if (SA == 4) {
@@ -1579,6 +1229,9 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
         if (red[q] > bm) bm = red[q];
         bnf |= rnf[q];
       }
+      // gl's error-norm term: the same constant at every cell (its K's are literal zeros)
+      if (a.evgl > bm) bm = a.evgl;
+      bnf |= !isfinite(a.evgl);
       if (bm > 0.0) atomicMax(a.eps_bits, (unsigned long long)__double_as_longlong(bm));
       if (bnf) atomicOr(a.nonfinite, 1u);
       if (a.pub) {
@@ -1790,10 +1443,7 @@ struct pft_slab {
   unsigned long long* sig;       // flag words written by the neighbours: [0] from below, [1] from
                                  // above (monotonic exchange sequence numbers); [8] put counter
   SlabPeer peer[2];              // [0] the neighbour below, [1] above
-  int fused_push;                // ipc: the fused kernels push (PFT_IPC_FUSED_PUSH, default 0)
   int drop_puts;                 // fault injection: halo puts and flag raises skipped (PFT_IPC_DROP_PUTS)
-  int pushed_role;               // buffer role whose boundary planes the last stage launch pushed
-                                 // into the neighbours (merson_fused), -1: none
   double* staging;       // host padded layout on the device (for upload/download)
   long S;                // host padded block (one field)
   unsigned long long* scratch;  // [0] eps bits, [1] nonfinite flag
@@ -1802,7 +1452,6 @@ struct pft_slab {
   unsigned long long* host_pub_dev;  // its device address
   hipStream_t stream, comm;
   hipStream_t side;      // error-norm read-back while the compute stream runs ahead
-  int launch_comm;       // 1: stage kernels go to the comm stream (the N > 1 boundary planes)
   hipEvent_t ev_order[3];  // stream-order events: [0] compute -> comm, [1] comm -> compute,
                            // [2] the last boundary launch on the comm stream
   hipEvent_t ev_eps;     // recorded on the compute stream after the error norm is final
@@ -1934,15 +1583,7 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
   s->tile_wx = 1;
   s->n1_tiled_ok = 1;
   s->recompute = 1;
-  s->pushed_role = -1;
   {
-    // ipc transport: 0 (default) = a separate put kernel after each stage; 1 = the fused stage
-    // kernels store their boundary planes into the neighbours after their z-march (PUSH
-    // instantiation).  Measured on the 400x400x100 / 318x318x159 / 252^3 / 200x200x400 rank slabs
-    // (scripts/ab_transport.sh, self exchange, two rounds): the put kernel cost 3-6% per rank, the
-    // push inside the stage kernels 5-9% (its boundary workgroups finish last)
-    const char* e = getenv("PFT_IPC_FUSED_PUSH");
-    s->fused_push = e ? atoi(e) : 0;
     // fault injection (tests/test_ipc_multiprocess.py): this slab never delivers its halo -- no
     // put, no flag raise -- as a peer that died would not
     const char* ed = getenv("PFT_IPC_DROP_PUTS");
@@ -1957,15 +1598,11 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
   }
   const size_t bytes = sizeof(double) * (3 * (size_t)s->fs + 2 * (size_t)s->plane);
   hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
-#if PFT_COMM_HIPRIO
   // the halo exchange's stream at the greatest priority: its RCCL kernel is dispatched ahead of
   // the interior sweep's workgroups when both become ready
   int prio_lo = 0, prio_hi = 0;
   if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   if (e == hipSuccess) e = hipStreamCreateWithPriority(&s->comm, hipStreamNonBlocking, prio_hi);
-#else
-  if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->comm, hipStreamNonBlocking);
-#endif
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&s->ev_eps, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&s->ev_order[0], hipEventDisableTiming);
@@ -2065,7 +1702,6 @@ static int ensure_staging(pft_slab* s)
 
 int pft_slab_upload_host(pft_slab* s, int which, const double* host_padded)
 {
-  s->pushed_role = -1;
   // X and XN may differ now: the caller re-establishes it (an upload of a stage buffer, e.g. A0
   // for a host-side RHS evaluation, leaves it alone)
   if (which == PFT_BUF_X || which == PFT_BUF_XN) s->gl_keep = 0;
@@ -2094,21 +1730,20 @@ int pft_slab_download_host(pft_slab* s, int which, double* host_padded)
 
 }  // extern "C"
 
-// kernel flavours: KCACHE (any n1, aux arrays), KTILE (LDS tile, aux arrays), KFUSED (LDS tile,
-// stage inputs recomputed from x and the K's -- the default for even n1)
-enum { KCACHE = 0, KTILE = 1, KFUSED = 2 };
+// kernel flavours: KCACHE (any n1, aux arrays), KFUSED (LDS tile, stage inputs recomputed from x
+// and the K's -- the default for even n1); 1 was the retired LDS-tiled aux-array kernel
+enum { KCACHE = 0, KFUSED = 2 };
 
 // resident workgroups per CU of the kernel launch_kernel would run (hipOccupancy..., cached)
 template <int STAGE, int MODE, bool GLS>
 static int kernel_occupancy(int kind, int wx)
 {
-  static int cache[3][2] = {{0, 0}, {0, 0}, {0, 0}};
-  int& n = cache[kind][(kind != KFUSED && wx == 16) ? 1 : 0];
+  static int cache[3] = {0, 0, 0};
+  (void)wx;
+  int& n = cache[kind];
   if (n) return n;
   const void* f = kind == KFUSED ? (const void*)merson_fused<STAGE, MODE, GLS>
-                : kind == KTILE ? (wx == 16 ? (const void*)merson_tile<STAGE, MODE, GLS, 16>
-                                            : (const void*)merson_tile<STAGE, MODE, GLS, 32>)
-                                : (const void*)merson_stage<STAGE, MODE, GLS>;
+                                 : (const void*)merson_stage<STAGE, MODE, GLS>;
   int b = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, kind == KFUSED ? PFT_FBLOCK : PFT_BLOCK, 0) != hipSuccess || b < 1) b = 1;
   n = b;
@@ -2143,18 +1778,7 @@ template <int STAGE, int MODE, bool GLS>
 static void launch_kernel(int kind, int wx, dim3 g, hipStream_t st, const StageArgs& a, const pft_consts& c)
 {
   if (kind == KFUSED) {
-    if constexpr (STAGE >= 1) {
-      if (a.plo || a.phi) {
-        merson_fused<STAGE, MODE, GLS, true><<<g, PFT_FBLOCK, 0, st>>>(a, c);
-        return;
-      }
-    }
     merson_fused<STAGE, MODE, GLS><<<g, PFT_FBLOCK, 0, st>>>(a, c);
-  } else if (kind == KTILE) {
-    if (wx == 16)
-      merson_tile<STAGE, MODE, GLS, 16><<<g, PFT_BLOCK, 0, st>>>(a, c);
-    else
-      merson_tile<STAGE, MODE, GLS, 32><<<g, PFT_BLOCK, 0, st>>>(a, c);
   } else {
     merson_stage<STAGE, MODE, GLS><<<g, PFT_BLOCK, 0, st>>>(a, c);
   }
@@ -2228,18 +1852,19 @@ static double fused_geometry(int n1, int n2, int* wx_out, int* ty_out)
 
 static int slab_kind(const pft_slab* s)
 {
-  if (s->d.n1 % 2 != 0 || s->tile_wx == 0) return KCACHE;   // 16-byte rows need n1 even
-  // automatic choice: the LDS-tiled kernels unless their tiles leave most lanes idle (planes
+  // 16-byte rows need n1 even; the aux-array path (recompute off) is the cache kernel's.  (An
+  // LDS-tiled aux-array kernel, 72 doubles per cell-step, was removed: measured slower than the
+  // recompute kernel everywhere)
+  if (s->d.n1 % 2 != 0 || s->tile_wx == 0 || !s->recompute) return KCACHE;
+  // automatic choice: the LDS-tiled kernel unless its tiles leave most lanes idle (planes
   // narrower than a tile, e.g. n1 < 32); the cache kernel's flat 256-cell workgroups fit any
   // plane.  Measured at 100^3 (50 x 50 x 100, 25 x 10-pair tiles fit exactly): 4 810 vs 3 980
   // Mcells*steps/s (47 vs 60 us per attempted step untimed)
-  if (s->tile_wx == 1 && s->recompute) {
+  if (s->tile_wx == 1) {
     int wx, ty;
     if (fused_geometry(s->d.n1, s->d.n2, &wx, &ty) < 0.7) return KCACHE;
-  } else if (s->tile_wx == 1 && (long)s->plane * s->d.n3 < 4L * s->n_cu * 3 * 512) {
-    return KCACHE;   // aux-array path, 64 x 8 / 32 x 16 tiles: the former size rule
   }
-  return s->recompute ? KFUSED : KTILE;
+  return KFUSED;
 }
 
 int pft_slab_stage_output(const pft_slab* s, int stage)
@@ -2261,8 +1886,8 @@ int pft_slab_tile_geometry(const pft_slab* s, int stage, int* wx, int* ty)
   } else if (kind == KFUSED && auto_tile) {
     fused_geometry(s->d.n1, s->d.n2, wx, ty);
   } else {
-    *wx = auto_tile ? (stage <= 2 ? 16 : 32) : s->tile_wx;
-    *ty = (kind == KFUSED ? PFT_FBLOCK : PFT_BLOCK) / *wx;
+    *wx = s->tile_wx;
+    *ty = PFT_FBLOCK / *wx;
   }
   return kind;
 }
@@ -2273,7 +1898,7 @@ int pft_slab_stage_fields(const pft_slab* s, int stage)
   // gl is not evolved under gl_static, and its K's are literal zeros on the recompute path
   if (stage < 1 || stage > 6) return -2;
   if (s->d.gl_static) return 2;
-  if (slab_kind(s) == KFUSED && PFT_GLK_LITERAL && stage != 5) return 2;
+  if (slab_kind(s) == KFUSED && stage != 5) return 2;
   // stage 5 with gl_keep (agreed by every rank, rk_solver.c): gl's x(t+h) is not stored; the
   // neighbours' XN gl ghost planes already equal X's (both exchanged at upload)
   if (stage == 5 && pft_slab_get_gl_keep(s) && slab_kind(s) == KFUSED) return 2;
@@ -2379,31 +2004,10 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   // stage-input coefficients of the recompute path: exactly the solver's h/3.0, h/6.0, h/8.0, h
   a.cin = stage == 2 ? h / 3.0 : stage == 3 ? h / 6.0 : stage == 4 ? h / 8.0 : h;
   if (kind == KFUSED && in) a.x = in;    // pure RHS / speculative stage 1: the input is the given buffer
-  // ipc transport: the fused kernel stores the output's boundary planes into the neighbours' ghost
-  // planes too (the buffer of the same role there: every rank swaps identically)
-  s->pushed_role = -1;
-  double* dst = stage == 5 ? out : kout;
-  if (kind == KFUSED && stage >= 1 && dst && s->fused_push && (s->peer[0].on || s->peer[1].on) && !bnd) {
-    int role = -1;
-    for (int r = 0; r < PFT_BUF_COUNT; ++r)
-      if (s->buf[r] == dst) role = r;
-    if (role >= 0) {
-      const int ph = s->phys[role];
-      if (s->peer[0].on) {
-        a.plo = s->peer[0].base[ph] + (long)(s->peer[0].n3 + 1) * s->plane;
-        a.plo_fs = s->peer[0].fs;
-      }
-      if (s->peer[1].on) {
-        a.phi = s->peer[1].base[ph];
-        a.phi_fs = s->peer[1].fs;
-      }
-      s->pushed_role = role;
-    }
-  }
   // gl's x(t+h) is x + coef*(0.5*(0.0 + 0.0) + 2.0*0.0) (gl's K's are literal zeros): equal to x
   // bit for bit when coef is finite and no gl value is -0.0 or NaN, which the solver checked at
   // upload (pft_slab_set_gl_keep); XN's gl then already holds it, and stage 5 skips that store
-  a.gl_keep = PFT_GL_KEEP && stage == 5 && kind == KFUSED && out && s->gl_keep && PFT_GLK_LITERAL && std::isfinite(coef) ? 1 : 0;
+  a.gl_keep = stage == 5 && kind == KFUSED && out && s->gl_keep && std::isfinite(coef) ? 1 : 0;
   a.em0 = s->d.eps_mult[0];
   a.em1 = s->d.eps_mult[1];
   a.em2 = s->d.eps_mult[2];
@@ -2420,7 +2024,7 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
     s->pub_slot = j;
   }
   dim3 g((unsigned)(a.ntile * a.nchunk));
-  const hipStream_t st = s->launch_comm ? s->comm : s->stream;
+  const hipStream_t st = s->stream;
   if (gls)
     launch_stage<true>(stage, mode, kind, wx, g, st, a, s->c);
   else
@@ -2460,7 +2064,7 @@ int pft_slab_set_gl_keep(pft_slab* s, int on)
   return 0;
 }
 
-int pft_slab_get_gl_keep(const pft_slab* s) { return PFT_GL_KEEP && PFT_GLK_LITERAL && s->gl_keep; }
+int pft_slab_get_gl_keep(const pft_slab* s) { return s->gl_keep; }
 
 int pft_slab_set_recompute(pft_slab* s, int on)
 {
@@ -2493,12 +2097,6 @@ int pft_slab_set_noise(pft_slab* s, const double* host_noise)
   return 0;
 }
 
-int pft_slab_launch_on_comm(pft_slab* s, int on)
-{
-  s->launch_comm = on ? 1 : 0;
-  return 0;
-}
-
 int pft_slab_order(pft_slab* s, int comm_first)
 {
   // the second stream waits for the work enqueued so far on the first
@@ -2506,16 +2104,6 @@ int pft_slab_order(pft_slab* s, int comm_first)
   hipEvent_t ev = s->ev_order[comm_first ? 1 : 0];
   HIPCHK(hipEventRecord(ev, from));
   HIPCHK(hipStreamWaitEvent(to, ev, 0));
-  return 0;
-}
-
-int pft_slab_boundary_event(pft_slab* s, int wait)
-{
-  if (wait) {
-    HIPCHK(hipStreamWaitEvent(s->stream, s->ev_order[2], 0));
-  } else {
-    HIPCHK(hipEventRecord(s->ev_order[2], s->comm));
-  }
   return 0;
 }
 
@@ -2682,29 +2270,29 @@ int pft_slab_stage_spec(pft_slab* s, double t_stage, int k_begin, int k_end)
 
 // ---- pair kernels (merson_pair): stages 2+3 and 4+5 of a step, one launch each -------------
 
-template <int SA, bool GLS>
+template <int SA, bool GLX>
 static void launch_pair_mode(int mode, dim3 g, hipStream_t st, const PairArgs& a, const pft_consts& c)
 {
   switch (mode) {
-    case 0: merson_pair<SA, 0, GLS><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
-    case 1: merson_pair<SA, 1, GLS><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
-    case 2: merson_pair<SA, 2, GLS><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
-    case 10: merson_pair<SA, 10, GLS><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
-    case 11: merson_pair<SA, 11, GLS><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
+    case 0: merson_pair<SA, 0, GLX><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
+    case 1: merson_pair<SA, 1, GLX><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
+    case 2: merson_pair<SA, 2, GLX><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
+    case 10: merson_pair<SA, 10, GLX><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
+    case 11: merson_pair<SA, 11, GLX><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
   }
 }
 
-template <int SA, bool GLS>
+template <int SA, bool GLX>
 static int pair_occupancy_mode(int mode)
 {
   static int cache[12] = {0};
   int& n = cache[mode];
   if (n) return n;
-  const void* f = mode == 0 ? (const void*)merson_pair<SA, 0, GLS>
-                : mode == 1 ? (const void*)merson_pair<SA, 1, GLS>
-                : mode == 2 ? (const void*)merson_pair<SA, 2, GLS>
-                : mode == 10 ? (const void*)merson_pair<SA, 10, GLS>
-                             : (const void*)merson_pair<SA, 11, GLS>;
+  const void* f = mode == 0 ? (const void*)merson_pair<SA, 0, GLX>
+                : mode == 1 ? (const void*)merson_pair<SA, 1, GLX>
+                : mode == 2 ? (const void*)merson_pair<SA, 2, GLX>
+                : mode == 10 ? (const void*)merson_pair<SA, 10, GLX>
+                             : (const void*)merson_pair<SA, 11, GLX>;
   int b = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, PFT_PBLOCK, 0) != hipSuccess || b < 1) b = 1;
   n = b;
@@ -2716,8 +2304,8 @@ static int pair_occupancy_mode(int mode)
 static bool pair_geometry_ok(int tx, int ty)
 {
   return tx >= 2 && tx % 2 == 0 && ty >= 1 && (tx / 2 + 2) * (ty + 4) <= PFT_PBLOCK &&
-         (tx + 4) * (ty + 4) + 2 * PFT_PAIR_PAD <= PFT_PAIR_LFA &&
-         (tx + 4) * (ty + 2) + 2 * PFT_PAIR_PAD <= PFT_PAIR_LFB;
+         tx + 4 <= PFT_PAIR_LP && PFT_PAIR_LP * (ty + 4) + 2 * PFT_PAIR_PAD <= PFT_PAIR_LFA &&
+         PFT_PAIR_LP * (ty + 2) + 2 * PFT_PAIR_PAD <= PFT_PAIR_LFB;
 }
 
 // automatic tile: the fewest workgroups per plane (a workgroup-plane costs about the same whatever
@@ -2745,6 +2333,24 @@ static long pair_geometry(int n1, int n2, int* tx_out, int* ty_out)
   *tx_out = bx;
   *ty_out = by;
   return best;
+}
+
+// gl's terms of a pair launch (its K's are the literal zeros of dgl, equation.c:731,874), each the
+// reference's expression with those zeros (hybrid2.c:388/428, 408/449, 521, 667), so every gl
+// value the kernel forms is the reference's bit for bit
+static void pair_gl_consts(PairArgs& a, int first, double em2)
+{
+  volatile double z = 0.0;    // evaluated at run time, operation by operation, like the kernels
+  const double k = z;
+  if (first == 2) {
+    a.glA = k * a.cinA;                                   // stage 2: K1 h/3 + x
+    a.glB = (k + k) * a.cinB;                             // stage 3: (K1 + K2) h/6 + x
+  } else {
+    a.glA = (k + 3.0 * k) * a.cinA;                       // stage 4: (K1 + 3 K3) h/8 + x
+    a.glB = (0.5 * k - 1.5 * k + 2.0 * k) * a.cinB;       // stage 5: (0.5 K1 - 1.5 K3 + 2 K4) h + x
+  }
+  a.glX = a.coef * (0.5 * (k + k) + 2.0 * k);             // x(t+h) = x + h/3 (0.5 (K1 + K5) + 2 K4)
+  a.evgl = em2 * fabs(0.2 * k - 0.9 * k + 0.8 * k - 0.1 * k);   // the error-norm term
 }
 
 static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, double coef, int k_begin,
@@ -2788,9 +2394,7 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
   } else {
     // z-chunks as run_stage's cost model: a chunk of kz planes evaluates stage A on kz + 2 and
     // loads kz + 3; `occ` workgroups per CU (one: 141 KiB of LDS)
-    const int gls = s->d.gl_static;
-    const int occ = first == 2 ? (gls ? pair_occupancy_mode<2, true>(mode) : pair_occupancy_mode<2, false>(mode))
-                               : (gls ? pair_occupancy_mode<4, true>(mode) : pair_occupancy_mode<4, false>(mode));
+    const int occ = first == 2 ? pair_occupancy_mode<2, false>(mode) : pair_occupancy_mode<4, false>(mode);
     int best_nch = 1;
     double best_cost = -1.0;
     for (int nch = 1; nch <= nplanes; ++nch) {
@@ -2819,9 +2423,12 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
   a.coef = coef;
   a.em0 = s->d.eps_mult[0];
   a.em1 = s->d.eps_mult[1];
-  a.em2 = s->d.eps_mult[2];
-  a.gl_keep = PFT_GL_KEEP && first == 4 && s->gl_keep && std::isfinite(coef) ? 1 : 0;
-  s->pushed_role = -1;
+  pair_gl_consts(a, first, s->d.eps_mult[2]);
+  // gl's inputs are x itself (GLX): gl_static, or gl_keep with finite coefficients, where
+  // glA + x == glB + x == x + glX == x for every gl value of x (no -0.0, no NaN: gl_clean)
+  const bool glx = s->d.gl_static ||
+                   (s->gl_keep && std::isfinite(a.cinA) && std::isfinite(a.cinB) && std::isfinite(coef));
+  a.gl_keep = glx ? 1 : 0;
   s->pub_armed = 0;
   if (first == 4 && s->inkernel_pub && !bnd && k_begin == 0 && k_end == s->d.n3) {
     const int j = (int)(s->pub_next % PFT_PUB_SLOTS);
@@ -2835,10 +2442,10 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
   const dim3 g((unsigned)(a.ntile * a.nchunk));
   const hipStream_t st = s->stream;
   if (first == 2) {
-    if (s->d.gl_static) launch_pair_mode<2, true>(mode, g, st, a, s->c);
+    if (glx) launch_pair_mode<2, true>(mode, g, st, a, s->c);
     else launch_pair_mode<2, false>(mode, g, st, a, s->c);
   } else {
-    if (s->d.gl_static) launch_pair_mode<4, true>(mode, g, st, a, s->c);
+    if (glx) launch_pair_mode<4, true>(mode, g, st, a, s->c);
     else launch_pair_mode<4, false>(mode, g, st, a, s->c);
   }
   HIPCHK(hipGetLastError());
@@ -2866,7 +2473,7 @@ int pft_slab_pair_ok(const pft_slab* s)
   const bool nb = s->d.has_below || s->d.has_above;
   if (nb && (s->d.n3 < 2 || s->noise)) return 0;
   // (merson_pair addresses a field with 32-bit byte offsets)
-  return PFT_GLK_LITERAL && s->pair_on && slab_kind(s) == KFUSED &&
+  return s->pair_on && slab_kind(s) == KFUSED &&
          (double)s->fs * 8.0 < 4294967296.0 && s->pair_ntile > 0;
 }
 
@@ -3031,13 +2638,6 @@ int pft_slab_halo_signal(pft_slab* s, unsigned long long seq)
   halo_signal_kernel<<<1, 64, 0, s->stream>>>(slo, shi, seq, s->peer[0].remote || s->peer[1].remote);
   HIPCHK(hipGetLastError());
   return 0;
-}
-
-int pft_slab_take_pushed(pft_slab* s, int role)
-{
-  const int r = s->pushed_role;
-  s->pushed_role = -1;
-  return r >= 0 && r == role;
 }
 
 int pft_slab_halo_wait(pft_slab* s, unsigned long long seq)

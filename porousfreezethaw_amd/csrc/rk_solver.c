@@ -40,7 +40,7 @@ typedef struct {
 	int *d_cs, *d_cz; double * d_cm; int d_nch, d_cap;
 	double *h_k, *h_aux; int h_cap;
 	/* options */
-	int opt_gls, opt_kz, opt_dev, opt_timing, opt_tile, opt_norecompute, opt_one_stream, opt_wave;
+	int opt_gls, opt_kz, opt_dev, opt_timing, opt_tile, opt_norecompute;
 	int opt_lazy;               /* PFT_OPT_LAZY_ALLOC: device buffers at the first solve, not at init */
 	int opt_pair;               /* PFT_OPT_PAIR: stages 2+3 and 4+5 as pair kernels where the slab can */
 	int deep;                   /* this call runs the pair kernels on z-neighbouring slabs: every stage
@@ -56,8 +56,7 @@ typedef struct {
 	pft_solver_stats stats;
 } solver_state;
 
-static __thread solver_state R = { .slab_dev = -1, .opt_kz = 0, .opt_dev = -1, .opt_tile = 1,
-                                   .opt_one_stream = 1, .opt_pair = 1 };
+static __thread solver_state R = { .slab_dev = -1, .opt_kz = 0, .opt_dev = -1, .opt_tile = 1, .opt_pair = 1 };
 
 static pft_comm * comm(void)
 {
@@ -161,8 +160,6 @@ int pft_solver_set_option(int opt, long value)
 		case PFT_OPT_KZ: if(value < 0) return -2; R.opt_kz = (int)value; if(R.slab) pft_slab_set_kz(R.slab, R.opt_kz); return 0;
 		case PFT_OPT_DEVICE: R.opt_dev = (int)value; return 0;
 		case PFT_OPT_TIMING: if(value < 0) return -2; R.opt_timing = (int)value; return 0;
-		case PFT_OPT_ONE_STREAM: if(value < 0 || value > 2) return -2; R.opt_one_stream = (int)value; return 0;
-		case PFT_OPT_WAVE: if(value < 0) return -2; R.opt_wave = (int)value; return 0;
 		case PFT_OPT_LAZY_ALLOC: R.opt_lazy = value ? 1 : 0; return 0;
 		case PFT_OPT_FAIL_RHS: if(value < 0) return -2; R.fail_rhs_after = value; R.rhs_calls = 0; return 0;
 		case PFT_OPT_PAIR: if(value < 0 || value > 2) return -2; R.opt_pair = (int)value; return 0;
@@ -287,54 +284,17 @@ static int do_stage(int stage, double ts, double coef, double h, long * launches
 		return rc;
 	}
 	/* SURVEY 8e.  Stage s reads the stage-(s-1) values of planes -1..n3 and writes its own; only
-	   its two boundary planes read ghost planes, so they are launched first and exchanged beside
-	   the interior sweep.  Default (one stream): boundary launch, the exchange on the comm stream
-	   beside the interior sweep, then the compute stream waits for the exchange.  Two streams
-	   (PFT_OPT_ONE_STREAM 0): the boundary launch and its exchange on the comm stream once the
-	   previous interior sweep is done; the interior sweep waits only for the previous stage's
-	   boundary launch. */
+	   its two boundary planes read ghost planes: they are launched first, exchanged on the comm
+	   stream beside the interior sweep, and the compute stream waits for the exchange before the
+	   next stage.  (Measured slower and removed: the boundary launch on the comm stream with the
+	   interior sweep waiting for it, and two-stream orders) */
 	n3 = R.slab_grid.n3;
-	if(R.opt_one_stream == 2) {
-		/* the boundary launch on the comm stream, its exchange right behind it in stream order (no
-		   cross-stream wait between them, so the priority stream's RCCL kernel is dispatched before
-		   the interior sweep, which waits for the boundary launch by event) */
-		if((rc = pft_slab_order(R.slab, 0))) return rc;          /* after the previous interior sweep */
-		pft_slab_launch_on_comm(R.slab, 1);
-		rc = run1(stage, ts, coef, h, PFT_K_BOUNDARY, 0);
-		pft_slab_launch_on_comm(R.slab, 0);
-		if(rc) return rc;
-		if((rc = pft_slab_boundary_event(R.slab, 0))) return rc; /* recorded behind the boundary launch */
-		if((rc = pft_comm_halo_enqueue_comm(c, out_buf, 0, nfields))) return rc;
-		if((rc = pft_slab_boundary_event(R.slab, 1))) return rc; /* the interior sweep waits for it */
-		if(n3 > 2 && (rc = run1(stage, ts, coef, h, 1, n3-1))) return rc;
-		if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
-		*launches += 2;
-		return 0;
-	}
-	if(R.opt_one_stream) {
-		/* one stream: both boundary planes, their exchange beside the interior sweep, then the
-		   compute stream waits for the exchange */
-		if((rc = run1(stage, ts, coef, h, PFT_K_BOUNDARY, 0))) return rc;
-		if((rc = pft_comm_halo_start(c, out_buf, 0, nfields))) return rc;
-		if(n3 > 2 && (rc = run1(stage, ts, coef, h, 1, n3-1))) return rc;
-		if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
-		*launches += 2;
-		return pft_comm_halo_finish(c);
-	}
-	if((rc = pft_slab_order(R.slab, 0))) return rc;
-	if((rc = pft_slab_boundary_event(R.slab, 1))) return rc;
-	/* the boundary launch is enqueued first: both launches become ready when the previous
-	   interior sweep ends, and the comm stream's (greatest-priority) workgroups go first */
-	pft_slab_launch_on_comm(R.slab, 1);
-	rc = run1(stage, ts, coef, h, PFT_K_BOUNDARY, 0);
-	pft_slab_launch_on_comm(R.slab, 0);
-	if(rc) return rc;
-	if((rc = pft_slab_boundary_event(R.slab, 0))) return rc;
-	if((rc = pft_comm_halo_enqueue_comm(c, out_buf, 0, nfields))) return rc;
+	if((rc = run1(stage, ts, coef, h, PFT_K_BOUNDARY, 0))) return rc;
+	if((rc = pft_comm_halo_start(c, out_buf, 0, nfields))) return rc;
 	if(n3 > 2 && (rc = run1(stage, ts, coef, h, 1, n3-1))) return rc;
 	if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
 	*launches += 2;
-	return 0;
+	return pft_comm_halo_finish(c);
 }
 
 /* stages first, first+1 (2+3 or 4+5) of the step as ONE pair kernel (pft_slab_pair; one slab):
@@ -362,35 +322,6 @@ static int do_pair(int first, double ta, double tb, double h, double coef, long 
 	if(rc || !R.deep) return rc;
 	/* between slabs (ipc): the whole slab, then the two-plane halo */
 	return pft_comm_halo_deep(c, out_buf, 0, pft_slab_stage_fields(R.slab, first+1));
-}
-
-/* PFT_OPT_WAVE = W > 0 (one slab, fused path): the five stages of a step as a skewed z-wavefront
-   of W-plane launches.  Chunk c runs stage s on planes [cW - (s-1), (c+1)W - (s-1)), so every
-   plane a stage reads from the stage before it (its z+1 neighbour included) was written by an
-   earlier launch, and the K a stage writes is read back one launch later, while it is still in
-   the 256 MB Infinity Cache.  Each buffer is written by one stage only (K1, A0 = K1 + K2, K3, K4,
-   XN), so no launch overwrites what a later launch of the step reads.  Same kernels, same
-   arithmetic per cell: bit-identical to one launch per stage. */
-static int wave_stages(int do1, double t, double h, double h2, double h3, double h6, double h8,
-                       long * launches)
-{
-	const double ts[6] = {0.0, t, t+h3, t+h3, t+h2, t+h};
-	const double cf[6] = {0.0, h3, h6, h8, h, h3};
-	const int n3 = R.slab_grid.n3, W = R.opt_wave;
-	int c, s, rc;
-	for(c = 0; c*W - 4 < n3; c++)
-		for(s = do1 ? 1 : 2; s <= 5; s++) {
-			const int kb = c*W - (s-1) < 0 ? 0 : c*W - (s-1);
-			const int ke = (c+1)*W - (s-1) > n3 ? n3 : (c+1)*W - (s-1);
-			if(kb >= ke) continue;
-			(*launches)++;
-			/* sampled timing: every launch of stages 2..5 (stage 1 is timed on the speculative
-			   launch, one per step) */
-			if(R.tstep && s > 1) pft_slab_timing_mark(R.slab, s, 0);
-			if((rc = pft_slab_stage(R.slab, s, ts[s], cf[s], h, kb, ke))) return rc;
-			if(R.tstep && s > 1) pft_slab_timing_mark(R.slab, s, 1);
-		}
-	return 0;
 }
 
 /* gl evolves by dgl == 0 (equation.c:731,874), so x(t+h) of gl is x + coef*0.0: x itself, bit for
@@ -447,7 +378,7 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	/* pair kernels (pft_slab_pair_ok: slab size, n3 >= 2 and no u_noise between slabs); every rank
 	   must take the same path -- the exchanges differ */
 	pft_slab_set_pair(R.slab, R.opt_pair);
-	pair = spec && R.opt_wave == 0 && pft_slab_pair_ok(R.slab);
+	pair = spec && pft_slab_pair_ok(R.slab);
 	if(nprocs > 1) {
 		long long no = !pair;
 		if((rc = pft_comm_allreduce_max_i64(c, &no))) return rc;
@@ -482,7 +413,7 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	   PFT_INKERNEL_PUBLISH=0 turns it off (A/B) */
 	{
 		const char * e = getenv("PFT_INKERNEL_PUBLISH");
-		const int on = spec && R.opt_wave == 0 && (!pft_comm_splits(c) || pft_comm_device_halo(c)) &&
+		const int on = spec && (!pft_comm_splits(c) || pft_comm_device_halo(c)) &&
 		               !(e && atoi(e) == 0);
 		pft_slab_set_inkernel_publish(R.slab, on);
 	}
@@ -493,10 +424,7 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 		/* the error norm accumulator is reset by its publication on the speculative path */
 		if((!spec || attempted == 0) && (rc = pft_slab_eps_reset(R.slab))) return rc;
 		/* K1 = f(t,x); aux = x + K1 h/3 ... K5 = f(t+h, aux); error norm; x(t+h) candidate */
-		if(R.opt_wave > 0 && spec && !pft_comm_splits(c)) {
-			/* the same five stages as a skewed z-wavefront of W-plane launches (wave_stages) */
-			if((rc = wave_stages(!k1_valid, t, h, h2, h3, h6, h8, &launches))) return rc;
-		} else if(pair) {
+		if(pair) {
 			/* the same arithmetic: stage A of each pair is evaluated inside stage B's stencil */
 			if(!k1_valid && (rc = do_stage(1, t, h3, h, &launches))) return rc;      /* :373-389 */
 			if((rc = do_pair(2, t+h3, t+h3, h, h3, &launches))) return rc;          /* :392-429 */

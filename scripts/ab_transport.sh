@@ -16,7 +16,6 @@ for round in 1 2; do
     set -- $dom
     run "$3_plain_r$round" --grid-nodes $1 --domain $2
     run "$3_ipc_r$round" --grid-nodes $1 --domain $2 --self-exchange --transport ipc
-    PFT_IPC_FUSED_PUSH=0 run "$3_ipcput_r$round" --grid-nodes $1 --domain $2 --self-exchange --transport ipc
     run "$3_rccl_r$round" --grid-nodes $1 --domain $2 --self-exchange --transport rccl
   done
   run "n1_callback_r$round" --callback

@@ -132,16 +132,19 @@ def test_full_size_reference_trajectory_bitwise(case, mode):
     sim.close()
 
 
-def test_400_four_slabs_reach_the_reference():
-    """configs[3]: 400^3 split 4-way (4 x 100 planes, loopback transport: the pair kernels with the
-    two-plane halo exchanged beside the interior launch), RK_MPI_SA_solve to the reference's g400
-    snapshot times (~45 and 67 attempted steps): every slab's t, h, counts and the assembled
-    fields equal the reference's bit for bit"""
+@pytest.mark.parametrize("pair", [1, 2])
+def test_400_four_slabs_reach_the_reference(pair):
+    """configs[3]: 400^3 split 4-way (4 x 100 planes, loopback transport), RK_MPI_SA_solve to the
+    reference's g400 snapshot times (~45 and 67 attempted steps): every slab's t, h, counts and the
+    assembled fields equal the reference's bit for bit.  pair 1: the automatic choice (a 4 M-cell
+    slab is below the pair kernels' threshold: one launch per stage, boundary planes first); 2: the
+    pair kernels forced, with the two-plane halo exchanged beside the interior launch"""
     meta, A = O.load_case("g400")
     Pm, info = O.params_from_meta({"params": meta["m0_params"]})
     times = meta["traj_m0_times"]
 
     def make(r):
+        P.lib().pft_solver_set_option(P.PFT_OPT_PAIR, pair)     # per host thread
         return P.Simulation(info["n1"], info["n2"], info["n3"], (info["L1"], info["L2"], info["L3"]), 0, Pm,
                             nprocs=4, rank=r, beads=O.beads(), tau=1.0, tau_min=info["tau_min"],
                             delta=info["delta"])
@@ -156,7 +159,7 @@ def test_400_four_slabs_reach_the_reference():
 
     out = M.loopback_run(4, make, run)
     assert [o[2] for o in out] == [100] * 4
-    assert all(o[3] == 1 for o in out)
+    assert all(o[3] == (pair == 2) for o in out)
     for i in range(len(times)):
         assert all(o[0][i] == out[0][0][i] for o in out)
         _check_golden(meta, A, 0, i, out[0][0][i], np.concatenate([o[1][i] for o in out], axis=1))

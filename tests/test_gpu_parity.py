@@ -23,8 +23,7 @@ def need_gpu():
 
 
 # kernel flavours: (tile width, recompute stage inputs)
-FLAVOURS = {"cache": (0, False), "tile32": (32, False), "tile16": (16, False),
-            "fused32": (32, True), "fused16": (16, True), "default": (1, True),
+FLAVOURS = {"cache": (0, False), "fused32": (32, True), "fused16": (16, True), "default": (1, True),
             "fusedauto": (2, True)}   # the fused kernel with the tile fitted to n1 x n2, at any size
 
 
@@ -126,7 +125,7 @@ def test_step_limited_resident_equals_continuous():
 # 100x36 -> 28x9
 @pytest.mark.parametrize("dims,flavour", [((30, 30, 60), "fused32"), ((30, 30, 60), "fused16"),
                                           ((66, 38, 21), "fused32"), ((17, 9, 13), "fused32"),
-                                          ((130, 70, 9), "fused16"), ((66, 38, 21), "tile32"),
+                                          ((130, 70, 9), "fused16"), ((66, 38, 21), "cache"),
                                           ((130, 70, 9), "cache"), ((50, 50, 20), "fusedauto"),
                                           ((252, 14, 6), "fusedauto"), ((318, 10, 5), "fusedauto"),
                                           ((130, 70, 9), "fusedauto"), ((66, 38, 21), "fusedauto"),
@@ -151,7 +150,7 @@ def test_matches_oracle_larger_grid(dims, flavour):
     sim.close()
 
 
-def _loopback_run(meta, initial, nprocs, times, mode=0, gl_static=False, flavour="fused32", one_stream=1):
+def _loopback_run(meta, initial, nprocs, times, mode=0, gl_static=False, flavour="fused32"):
     L = P.lib()
     group = C.c_void_p()
     assert L.pft_comm_init_loopback(C.byref(group), nprocs) == 0
@@ -162,7 +161,6 @@ def _loopback_run(meta, initial, nprocs, times, mode=0, gl_static=False, flavour
             mine = C.c_void_p()
             assert L.pft_comm_loopback_rank(group, r, C.byref(mine)) == 0
             L.pft_comm_set_current(mine)
-            L.pft_solver_set_option(P.PFT_OPT_ONE_STREAM, one_stream)   # per host thread
             Pm, info = O.params_from_meta(meta)
             sim = P.Simulation(info["n1"], info["n2"], info["n3"], (info["L1"], info["L2"], info["L3"]), mode,
                                Pm, nprocs=nprocs, rank=r, initial=initial, tau=1.0, tau_min=info["tau_min"],
@@ -190,17 +188,15 @@ def _loopback_run(meta, initial, nprocs, times, mode=0, gl_static=False, flavour
     return out
 
 
-@pytest.mark.parametrize("one_stream", [1, 0, 2])
 @pytest.mark.parametrize("nprocs", [2, 4])
 @pytest.mark.parametrize("gl_static", [False, True])
-@pytest.mark.parametrize("flavour", ["default", "fused32", "tile16", "cache"])
-def test_multislab_loopback_bitwise(nprocs, gl_static, flavour, one_stream):
+@pytest.mark.parametrize("flavour", ["default", "fused32", "fused16", "cache"])
+def test_multislab_loopback_bitwise(nprocs, gl_static, flavour):
     """Z-slab decomposition with halo exchange (boundary planes first, interior overlapped) over
     the loopback transport on one GPU: identical to the single-slab reference trajectory (F6)"""
     meta, A = O.load_case("g20")
     times = meta["traj_times"][:2]
-    out = _loopback_run(meta, A["traj_m0_ic"], nprocs, times, gl_static=gl_static, flavour=flavour,
-                        one_stream=one_stream)
+    out = _loopback_run(meta, A["traj_m0_ic"], nprocs, times, gl_static=gl_static, flavour=flavour)
     for i in range(len(times)):
         ref = meta["traj_m0"][i]
         for r in range(nprocs):
@@ -221,10 +217,9 @@ def _self_exchange_comm():
     return comm
 
 
-@pytest.mark.parametrize("one_stream", [1, 0, 2])
 @pytest.mark.parametrize("gl_static", [False, True])
-@pytest.mark.parametrize("flavour", ["default", "fusedauto", "fused16", "tile32", "cache"])
-def test_rccl_stage_pipeline_self_exchange_bitwise(gl_static, flavour, one_stream):
+@pytest.mark.parametrize("flavour", ["default", "fusedauto", "fused16", "fused32", "cache"])
+def test_rccl_stage_pipeline_self_exchange_bitwise(gl_static, flavour):
     """the N > 1 stage pipeline through real RCCL calls on one GPU (pft_comm_set_self_exchange):
     both boundary planes in one launch, ncclSend/ncclRecv on the priority comm stream beside the
     interior sweep, the eps max by ncclAllReduce and its publication on the comm stream.  The
@@ -233,7 +228,6 @@ def test_rccl_stage_pipeline_self_exchange_bitwise(gl_static, flavour, one_strea
     L = P.lib()
     comm = _self_exchange_comm()
     L.pft_comm_set_current(comm)
-    L.pft_solver_set_option(P.PFT_OPT_ONE_STREAM, one_stream)
     try:
         meta, A = O.load_case("g20")
         sim, Pm, info = make_sim(meta, A["traj_m0_ic"], mode=0, gl_static=gl_static, flavour=flavour)
@@ -245,7 +239,6 @@ def test_rccl_stage_pipeline_self_exchange_bitwise(gl_static, flavour, one_strea
             assert np.array_equal(sim.interior(), A[f"traj_m0_state{i}"])
         sim.close()
     finally:
-        L.pft_solver_set_option(P.PFT_OPT_ONE_STREAM, 1)
         L.pft_comm_set_current(None)
         L.pft_comm_destroy(comm)
 
@@ -393,7 +386,7 @@ def test_snapshot_restart_continues_trajectory(tmp_path):
 
 
 @pytest.mark.parametrize("mode", [0, 1, 10, 11])
-@pytest.mark.parametrize("flavour", ["default", "fused32", "tile16", "cache"])
+@pytest.mark.parametrize("flavour", ["default", "fused32", "fused16", "cache"])
 def test_rhs_with_temperature_noise(mode, flavour):
     """u_noise (u_noise_amp != 0, equation.c:450-456, 676-687): the device RHS with the slab's
     noise field equals the oracle's stencil given the same field"""
@@ -417,79 +410,6 @@ def test_rhs_with_temperature_noise(mode, flavour):
     dwo = np.zeros_like(w)
     O.lib().pft_or_stencil(C.byref(g), O.ptr(Pm), mode, O.ptr(w), O.ptr(noise), O.ptr(dwo))
     assert np.array_equal(K, O.unpad(g, dwo))
-
-
-@pytest.mark.parametrize("wave", [1, 3, 7])
-@pytest.mark.parametrize("gl_static", [False, True])
-@pytest.mark.parametrize("flavour", ["default", "fusedauto", "fused16", "fused32", "cache"])
-def test_wavefront_schedule_bitwise(wave, gl_static, flavour):
-    """PFT_OPT_WAVE (rk_solver.c wave_stages): a step's five stages as a skewed z-wavefront of
-    W-plane launches reach the reference trajectory bit for bit.  The cache kernel has no
-    recompute path and keeps one launch per stage; so does "default" here, which picks the cache
-    kernel for the 10-cell-wide g20 plane"""
-    L = P.lib()
-    assert L.pft_solver_set_option(P.PFT_OPT_WAVE, wave) == 0
-    try:
-        meta, A = O.load_case("g20")
-        sim, Pm, info = make_sim(meta, A["traj_m0_ic"], mode=0, gl_static=gl_static, flavour=flavour)
-        for i, T in enumerate(meta["traj_times"][:2]):
-            rc = sim.solve(T)
-            ref = meta["traj_m0"][i]
-            assert (sim.t.hex(), sim.h.hex(), sim.system.steps, sim.system.steps_total, rc) == \
-                (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(), ref[2], ref[3], ref[4])
-            assert np.array_equal(sim.interior(), A[f"traj_m0_state{i}"])
-        st = sim.stats()
-        if flavour not in ("cache", "default"):
-            assert st.kernel_launches > 6 * st.steps_total
-        else:
-            assert st.kernel_launches == 5 * st.steps_total
-        sim.close()
-    finally:
-        L.pft_solver_set_option(P.PFT_OPT_WAVE, 0)
-
-
-def test_wavefront_schedule_larger_grid():
-    """the wavefront on a 100 x 36 x 40 grid (W = 6: clipped first and last chunks, several
-    z-chunks per launch) vs the oracle, 12 attempted steps"""
-    L = P.lib()
-    assert L.pft_solver_set_option(P.PFT_OPT_WAVE, 6) == 0
-    try:
-        meta, A = O.load_case("g20")
-        Pm, info = O.params_from_meta(meta)
-        n1, n2, n3 = 100, 36, 40
-        info = dict(info, n1=n1, n2=n2, n3=n3)
-        sim = P.Simulation(n1, n2, n3, (info["L1"], info["L2"], info["L3"]), 0, Pm, beads=O.beads(), tau=1.0,
-                           tau_min=info["tau_min"], delta=info["delta"], tile=2)
-        ic = sim.interior()
-        assert sim.solve_ex(1e9, 12, 0) == 2
-        res = O.solve(info, Pm, 0, ic, 0.0, 1.0, [1e9], max_steps_total=12)[0]
-        assert (sim.t, sim.h, sim.system.steps, sim.system.steps_total) == (res[0], res[1], res[2], res[3])
-        assert np.array_equal(sim.interior(), res[5])
-        sim.close()
-    finally:
-        L.pft_solver_set_option(P.PFT_OPT_WAVE, 0)
-
-
-def test_full_size_400_wavefront_bitwise():
-    """400^3 at full size: 3 attempted steps as a skewed z-wavefront of 24-plane launches equal the
-    one-launch-per-stage run bit for bit"""
-    base, Pm, info = _full_size_case()
-    L3s = (info["L1"], info["L2"], info["L3"])
-    L = P.lib()
-    outs = []
-    for wave in (0, 24):
-        assert L.pft_solver_set_option(P.PFT_OPT_WAVE, wave) == 0
-        try:
-            s = P.Simulation(info["n1"], info["n2"], info["n3"], L3s, 0, Pm, beads=O.beads(), tau=1.0,
-                             tau_min=info["tau_min"], delta=info["delta"])
-            assert s.solve_ex(1e9, 3, 0) == 2
-            outs.append(((s.t, s.h, s.system.steps, s.system.steps_total), s.interior(), s.stats().kernel_launches))
-            s.close()
-        finally:
-            L.pft_solver_set_option(P.PFT_OPT_WAVE, 0)
-    assert outs[0][0] == outs[1][0]
-    assert np.array_equal(outs[0][1], outs[1][1])
-    assert outs[1][2] > outs[0][2]
 
 
 @pytest.mark.parametrize("flavour", ["default", "fusedauto"])

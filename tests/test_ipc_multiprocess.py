@@ -34,14 +34,12 @@ def need_gpu():
         pytest.fail("no HIP device: the gpu tests must run on an MI355X (no CPU fallback exists)")
 
 
-def _run_ranks(tmp_path, nranks, timeout=240, push=None, rank_env=None, ipc_timeout="120", **spec):
+def _run_ranks(tmp_path, nranks, timeout=240, rank_env=None, ipc_timeout="120", **spec):
     spec = dict(spec, nranks=nranks, shm=f"/pft_test_{os.getpid()}_{uuid.uuid4().hex[:12]}",
                 out=str(tmp_path / "rank"))
     path = tmp_path / "spec.json"
     path.write_text(json.dumps(spec))
     env = dict(os.environ, PFT_IPC_TIMEOUT=ipc_timeout)
-    if push is not None:
-        env["PFT_IPC_FUSED_PUSH"] = str(push)     # 1: the stage kernels store the boundary planes
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "_ipc_worker.py"), str(path), str(r)],
                               env=dict(env, **((rank_env or {}).get(r, {}))), stdout=subprocess.PIPE,
                               stderr=subprocess.STDOUT) for r in range(nranks)]
@@ -59,14 +57,13 @@ def _run_ranks(tmp_path, nranks, timeout=240, push=None, rank_env=None, ipc_time
     return [dict(np.load(f"{spec['out']}.{r}.npz")) for r in range(nranks)]
 
 
-@pytest.mark.parametrize("nranks,tile,push", [(2, None, None), (3, 32, None), (4, None, None), (4, 32, None),
-                                               (3, 32, 1), (2, 2, 1)])
-def test_g20_processes_equal_reference(tmp_path, nranks, tile, push):
-    """push 1: the fused kernels (tile 32 / 2) store their boundary planes into the neighbours'
-    ghost planes themselves instead of the separate put kernel"""
+@pytest.mark.parametrize("nranks,tile", [(2, None), (3, 32), (4, None), (4, 32), (2, 2)])
+def test_g20_processes_equal_reference(tmp_path, nranks, tile):
+    """tile 32 / 2: the fused kernels with fixed / fitted tiles (the default picks the cache
+    kernel for the 10-cell-wide plane)"""
     meta, A = O.load_case("g20")
     times = meta["traj_times"]
-    res = _run_ranks(tmp_path, nranks, case="g20", times=times, tile=tile, push=push)
+    res = _run_ranks(tmp_path, nranks, case="g20", times=times, tile=tile)
     for r in res:
         assert int(r["path"]) == 1
     for i in range(len(times)):
