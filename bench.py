@@ -363,9 +363,28 @@ def slab_digest(sim):
     if os.environ.get("PFT_BENCH_PARITY_PERTURB") == str(g.rank):
         # diagnostic: one value of this rank's state off by one ulp, so that the check must fail
         x.reshape(-1)[x.size // 2] = np.nextafter(x.reshape(-1)[x.size // 2], np.inf)
-    return {"t": float(sim.t).hex(), "h": float(sim.h).hex(), "steps": int(sim.system.steps),
-            "steps_total": int(sim.system.steps_total), "first_row": int(g.first_row), "n3": int(g.n3),
-            "sha256": hashlib.sha256(x.tobytes()).hexdigest()}
+    return slab_record(x, sim.t, sim.h, sim.system.steps, sim.system.steps_total, g.first_row, g.n3)
+
+
+def slab_record(x, t, h, steps, steps_total, first_row, n3):
+    """what a rank hands to rank 0 for the parity check: (t, h, steps, steps_total) exactly, its
+    Z-slab's place, and the SHA-256 of its interior state x[field][k][j][i]"""
+    return {"t": float(t).hex(), "h": float(h).hex(), "steps": int(steps), "steps_total": int(steps_total),
+            "first_row": int(first_row), "n3": int(n3),
+            "sha256": hashlib.sha256(np.ascontiguousarray(x).tobytes()).hexdigest()}
+
+
+def compare_records(ranks, x, t, h, steps, steps_total):
+    """every rank's record against the single-slab state x (all planes) and trajectory position:
+    the list of mismatching ranks and fields (empty: the decomposition changed no bit)"""
+    bad = []
+    for r, m in enumerate(ranks):
+        f, n = m["first_row"], m["n3"]
+        want = slab_record(x[:, f:f + n], t, h, steps, steps_total, f, n)
+        diff = [k for k in want if want[k] != m[k]]
+        if diff:
+            bad.append({"rank": r, "fields": diff})
+    return bad
 
 
 def parity_check(ranks, calls, a, base, dims, Ls, beads, final_time, dev):
@@ -389,15 +408,7 @@ def parity_check(ranks, calls, a, base, dims, Ls, beads, final_time, dev):
     ref.download()
     x = ref.interior()
     pairs = bool(ref.stats().pairs)
-    bad = []
-    for r, m in enumerate(ranks):
-        f, n = m["first_row"], m["n3"]
-        want = {"t": float(ref.t).hex(), "h": float(ref.h).hex(), "steps": int(ref.system.steps),
-                "steps_total": int(ref.system.steps_total),
-                "sha256": hashlib.sha256(np.ascontiguousarray(x[:, f:f + n]).tobytes()).hexdigest()}
-        diff = [k for k in want if want[k] != m[k]]
-        if diff:
-            bad.append({"rank": r, "fields": diff})
+    bad = compare_records(ranks, x, ref.t, ref.h, ref.system.steps, ref.system.steps_total)
     ref.close()
     return {"equal": not bad, "attempted_steps": int(sum(calls)), "calls": calls, "ranks": len(ranks),
             "reference": "one slab on rank 0's GPU, same initial condition and solve calls"

@@ -6,8 +6,11 @@ RCCL grouped send/recv, pft_comm.hip) and takes one max-allreduce of the error n
 attempted step (RK_MPI_SAsolver_hybrid2.c:572).  Here two processes run that protocol over
 torch.distributed/gloo around the CPU oracle's Merson loop, and the gathered result must equal
 the reference's single-rank trajectory bit for bit (the reference is rank-count invariant,
-SURVEY F6).  The libpft side of the same protocol (RCCL / loopback transports) is covered on the
-GPU by tests/test_gpu_parity.py (loopback multi-slab cases).
+SURVEY F6).  This is the oracle's protocol, not libpft's: libpft needs a GPU for every solve.
+libpft's own cross-process path is tests/test_ipc_multiprocess.py (2-4 processes over the ipc
+transport, GPU), its threads-in-one-process path the loopback cases of test_gpu_parity.py /
+test_pair_gpu.py, and its RCCL calls the 1-rank self-exchange cases; the bench's gloo-side
+decomposition parity check is test_bench_parity_gloo below.
 """
 import ctypes as C
 import os
@@ -29,7 +32,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, mode, T, outdir):
+def _worker(rank, world, port, mode, T, outdir, parity=None):
     import torch
     import torch.distributed as dist
     sys.path.insert(0, HERE)
@@ -75,6 +78,25 @@ def _worker(rank, world, port, mode, T, outdir):
                                info["delta"], 0, Ow.ptr(x), C.byref(s), C.byref(st), 0, ex, ar, None)
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), x=Ow.unpad(g, x),
              ctl=np.array([t.value, h.value, s.value, st.value, rc], dtype=np.float64))
+    if parity is not None:
+        # bench.py --gpus N's decomposition check, as its ranks run it: every rank hands rank 0 its
+        # record (all_gather_object), rank 0 compares them with the single-slab state -- here the
+        # reference's own golden state; `parity` names a rank whose state is put off by one ulp
+        sys.path.insert(0, REPO)
+        import json
+        import bench
+        mine = Ow.unpad(g, x)
+        if parity == rank:
+            mine.reshape(-1)[mine.size // 2] = np.nextafter(mine.reshape(-1)[mine.size // 2], np.inf)
+        rec = bench.slab_record(mine, t.value, h.value, s.value, st.value, g.first_row, g.n3)
+        ranks = [None] * world
+        dist.all_gather_object(ranks, rec)
+        if rank == 0:
+            ref = meta[f"traj_m{mode}"][0]
+            bad = bench.compare_records(ranks, A[f"traj_m{mode}_state0"], float.fromhex(ref[0]),
+                                        float.fromhex(ref[1]), ref[2], ref[3])
+            with open(os.path.join(outdir, "parity.json"), "w") as f:
+                json.dump(bad, f)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -94,6 +116,23 @@ def test_two_rank_trajectory_equals_single_rank_reference(tmp_path, mode):
         assert (t.hex(), h.hex(), int(s), int(st), int(rc)) == (
             float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(), ref[2], ref[3], ref[4])
     assert np.array_equal(x, A[f"traj_m{mode}_state0"])
+
+
+@pytest.mark.parametrize("perturb", [-1, 1])
+def test_bench_parity_gloo(tmp_path, perturb):
+    """bench.py's N > 1 self-check over gloo with 2 ranks: the gathered per-rank records equal the
+    single-slab (reference) state when the run is right, and name the rank that is one ulp off
+    when it is not"""
+    import json
+    mp = pytest.importorskip("torch.multiprocessing")
+    meta, A = O.load_case("g20")
+    T = meta["traj_times"][0]
+    mp.spawn(_worker, args=(2, _free_port(), 0, T, str(tmp_path), perturb), nprocs=2, join=True)
+    bad = json.load(open(tmp_path / "parity.json"))
+    if perturb < 0:
+        assert bad == []
+    else:
+        assert bad == [{"rank": perturb, "fields": ["sha256"]}]
 
 
 def test_decomposition_matches_reference_rule():
