@@ -227,10 +227,57 @@ struct StageArgs {
   // the host) and resets the accumulator; pub_count counts the finished workgroups
   unsigned long long* pub;
   unsigned int* pub_count;
+  struct EpsShard* shards;   // stage 5: the error norm's per-shard accumulators (eps_arrive)
 };
 
 // a value the error norm never takes (a NaN pattern: the max skips NaN) nor the flag
 #define PFT_PUB_SENTINEL 0xFFF8DEADBEEF0001ULL
+
+// The error norm's max over the workgroups of a launch (hybrid2.c:507-524 over the slab), and with
+// it the count of finished workgroups whose last one publishes: arrivals on one address serialise
+// at the memory side (~12 ns each), so a launch of ~500 short workgroups that all finish at once
+// spent ~6 us in that queue (stage 5 at 100^3: 13.5 against 7 us for stage 4).  Workgroups
+// arrive on one of PFT_EPS_SHARDS shards (blockIdx % shards: the dispatcher deals consecutive
+// blocks to different XCDs) and the last of each shard forwards its shard's max to the launch's
+// accumulator -- the same max, a tenth of the queue.  Every word is reset by the workgroup that
+// reads it last, so the next launch on the stream finds them zero.
+#define PFT_EPS_SHARDS 8
+struct EpsShard {
+  unsigned long long max;   // bit pattern of the shard's max (non-negative doubles order as their bits)
+  unsigned int nf, cnt;     // non-finite flag, finished workgroups
+  unsigned long long pad[6];  // one 64-byte line per shard
+};
+
+// called by one thread per workgroup after its block-level max bm / flag bnf; pub: the pinned host
+// slot of an in-kernel publication (null: the accumulator is read after the launch)
+__device__ __forceinline__ void eps_arrive(double bm, int bnf, EpsShard* shards, unsigned long long* eps_bits,
+                                           unsigned int* nonfinite, unsigned long long* pub, unsigned int* pub_count)
+{
+  const unsigned nb = gridDim.x, b = blockIdx.x % PFT_EPS_SHARDS;
+  const unsigned nsh = nb < PFT_EPS_SHARDS ? nb : PFT_EPS_SHARDS;             // shards with workgroups
+  const unsigned in_shard = (nb - b + PFT_EPS_SHARDS - 1) / PFT_EPS_SHARDS;   // workgroups of shard b
+  EpsShard* sh = shards + b;
+  if (bm > 0.0) atomicMax(&sh->max, (unsigned long long)__double_as_longlong(bm));   // NaN never wins
+  if (bnf) atomicOr(&sh->nf, 1u);
+  // this workgroup's atomics are performed (memory-side) before it is counted
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (atomicAdd(&sh->cnt, 1u) != in_shard - 1) return;
+  const unsigned long long m = atomicExch(&sh->max, 0ULL);
+  const unsigned int f = atomicExch(&sh->nf, 0u);
+  atomicExch(&sh->cnt, 0u);
+  if (m) atomicMax(eps_bits, m);
+  if (f) atomicOr(nonfinite, 1u);
+  if (!pub) return;
+  // the last shard to finish reads the final max, resets the accumulator and publishes both words
+  // to the host, which polls them (no publish kernel, no event: pft_slab_eps_fetch)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (atomicAdd(pub_count, 1u) != nsh - 1) return;
+  const unsigned long long e = atomicExch(eps_bits, 0ULL);
+  const unsigned int ff = atomicExch(nonfinite, 0u);
+  atomicExch(pub_count, 0u);
+  __hip_atomic_store(pub, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(pub + 1, (unsigned long long)ff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 
 __device__ __forceinline__ int xcd_remap(int b, int n)
@@ -755,21 +802,7 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
         if (red[q] > bm) bm = red[q];
         bnf |= rnf[q];
       }
-      if (bm > 0.0) atomicMax(a.eps_bits, (unsigned long long)__double_as_longlong(bm));
-      if (bnf) atomicOr(a.nonfinite, 1u);
-      if (a.pub) {
-        // this workgroup's atomics are performed (memory-side) before it is counted; the last one
-        // counted reads the final max, resets the accumulator and publishes both words to the
-        // host, which polls them (no publish kernel, no event: pft_slab_eps_fetch)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (atomicAdd(a.pub_count, 1u) == gridDim.x - 1) {
-          const unsigned long long e = atomicExch(a.eps_bits, 0ULL);
-          const unsigned int f = atomicExch(a.nonfinite, 0u);
-          atomicExch(a.pub_count, 0u);
-          __hip_atomic_store(a.pub, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_store(a.pub + 1, (unsigned long long)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      }
+      eps_arrive(bm, bnf, a.shards, a.eps_bits, a.nonfinite, a.pub, a.pub_count);
     }
   }
 }
@@ -820,6 +853,7 @@ struct PairArgs {
   unsigned int* nonfinite;
   unsigned long long* pub;   // in-kernel publication of the error norm (as merson_fused<5>)
   unsigned int* pub_count;
+  EpsShard* shards;    // the error norm's per-shard accumulators (eps_arrive)
   long fs;
   int n1, n2, n3, plane;
   int has_below, has_above;   // z-neighbours: stage A also runs on the ghost plane next to each,
@@ -1083,7 +1117,11 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
       PFT_PAIR_BIND(A0, C0);
       (void)C0;
       // stage A's input of plane mm + 1 (own pair: read back by this thread in this iteration;
-      // x/y neighbours: in the next one, behind the barrier)
+      // x/y neighbours: in the next one, behind the barrier), and the look-ahead load of plane
+      // mm + 2.  Both unconditional -- beyond mlast the load re-reads plane mlast and the store
+      // lands in the ring slot of plane mm - 2, which nobody reads any more -- so that no branch
+      // separates a load from its use: with the loads under a branch the compiler's s_waitcnt
+      // placement lost track of them and stage A waited for the look-ahead it had just issued.
       if (mm + 1 <= mlast) {
 #pragma unroll
         for (int q = 0; q < 3; ++q) st2x(&lA[sAp][q][posA], pair_in_A<SA, GLX>(A0, q, rn), xsw);
@@ -1142,6 +1180,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
       // operands of plane kB for stage B's outputs (4+5), after stage A: fewer registers live
       // during stage A, and the latency hides behind stage B's stencil
       // (GLX: gl's x(t+h) is not stored, XN holds it: gl's x is not needed)
+      // (unconditional, as the look-ahead: every lane's acting pair is in the domain)
       if (SA == 4 && kB >= kb && isB) pair_load<SA, !GLX>(A2, pbo(kB), ro);
       if (kB >= kb && isB) {
         constexpr int sB = (PH + 2) % 3, sBm = (PH + 1) % 3, sBp = PH;   // slots of planes kB, kB-1, kB+1
@@ -1232,18 +1271,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
       // gl's error-norm term: the same constant at every cell (its K's are literal zeros)
       if (a.evgl > bm) bm = a.evgl;
       bnf |= !isfinite(a.evgl);
-      if (bm > 0.0) atomicMax(a.eps_bits, (unsigned long long)__double_as_longlong(bm));
-      if (bnf) atomicOr(a.nonfinite, 1u);
-      if (a.pub) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (atomicAdd(a.pub_count, 1u) == gridDim.x - 1) {
-          const unsigned long long e = atomicExch(a.eps_bits, 0ULL);
-          const unsigned int f = atomicExch(a.nonfinite, 0u);
-          atomicExch(a.pub_count, 0u);
-          __hip_atomic_store(a.pub, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_store(a.pub + 1, (unsigned long long)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      }
+      eps_arrive(bm, bnf, a.shards, a.eps_bits, a.nonfinite, a.pub, a.pub_count);
     }
   }
 }
@@ -1463,6 +1491,7 @@ struct pft_slab {
   unsigned long long* pub_ring;      // host address (PFT_PUB_SLOTS x 2 words)
   unsigned long long* pub_ring_dev;  // its device address
   unsigned int* pub_count;           // device: finished workgroups of the publishing launch
+  EpsShard* eps_shards;              // device: the error norm's shards (after pub_count's line)
   long pub_next;                     // slots used so far
   int pub_armed;                     // the last stage-5 launch publishes into slot pub_slot
   int pub_slot;
@@ -1615,8 +1644,10 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
   if (e == hipSuccess)
     e = hipHostMalloc((void**)&s->pub_ring, 16 * PFT_PUB_SLOTS, hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&s->pub_ring_dev, s->pub_ring, 0);
-  if (e == hipSuccess) e = hipMalloc((void**)&s->pub_count, 64);
-  if (e == hipSuccess) e = hipMemsetAsync(s->pub_count, 0, 64, s->stream);
+  const size_t cnt_bytes = 64 + sizeof(EpsShard) * PFT_EPS_SHARDS;
+  if (e == hipSuccess) e = hipMalloc((void**)&s->pub_count, cnt_bytes);
+  if (e == hipSuccess) e = hipMemsetAsync(s->pub_count, 0, cnt_bytes, s->stream);
+  if (e == hipSuccess) s->eps_shards = (EpsShard*)((char*)s->pub_count + 64);
   // the flag words are polled by the command processor (hipStreamWaitValue64) and written by a
   // neighbour -- possibly another GPU over xGMI: uncached device memory, so that no cache between
   // the writer and the poller can hold a stale copy
@@ -1933,6 +1964,7 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   a.out = out;
   a.noise = s->noise;
   a.eps_bits = s->scratch;
+  a.shards = s->eps_shards;
   a.nonfinite = (unsigned int*)(s->scratch + 1);
   a.fs = s->fs;
   a.n1 = s->d.n1;
@@ -2368,6 +2400,7 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
   a.out = (first == 2 ? s->buf[PFT_BUF_K3] : s->buf[PFT_BUF_XN]) - s->plane;
   a.noise = s->noise;
   a.eps_bits = s->scratch;
+  a.shards = s->eps_shards;
   a.nonfinite = (unsigned int*)(s->scratch + 1);
   a.fs = s->fs;
   a.n1 = s->d.n1;
