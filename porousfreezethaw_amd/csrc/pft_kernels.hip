@@ -228,6 +228,10 @@ struct StageArgs {
   unsigned long long* pub;
   unsigned int* pub_count;
   struct EpsShard* shards;   // stage 5: the error norm's per-shard accumulators (eps_arrive)
+  // deferred publication (eps_reduce_publish): stage 5 stores its workgroups' partials to part;
+  // stage 1 with npart > 0 reduces npart partials in its last workgroup and publishes them to pub
+  unsigned long long* part;
+  int npart;
 };
 
 // a value the error norm never takes (a NaN pattern: the max skips NaN) nor the flag
@@ -277,6 +281,57 @@ __device__ __forceinline__ void eps_arrive(double bm, int bnf, EpsShard* shards,
   atomicExch(pub_count, 0u);
   __hip_atomic_store(pub, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(pub + 1, (unsigned long long)ff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Deferred publication (single slab / ipc, the speculative path): the error-norm launch does no
+// atomics at all -- each workgroup stores its (max bits, non-finite flag) to part[2 b], part[2 b + 1]
+// -- and the NEXT launch on the stream, the speculative stage 1, which follows it in every step,
+// reduces them in one extra workgroup and publishes to the pinned host slot while its other
+// workgroups compute.  The reduction leaves the error-norm launch's critical path (its last
+// workgroups spent ~1-2 us in the arrival atomics), and the kernel boundary orders the plain stores
+// before the reads.  One block of 256 threads; called with the block's threads.
+__device__ __forceinline__ void eps_reduce_publish(const unsigned long long* __restrict__ part, int n,
+                                                   unsigned long long* pub)
+{
+  __shared__ unsigned long long rm[4], rf[4];
+  unsigned long long m = 0, f = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const unsigned long long b = part[2 * i], nf = part[2 * i + 1];
+    m = b > m ? b : m;   // non-negative doubles (and +0) order as their bit patterns
+    f |= nf;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long om = __shfl_xor(m, off, 64), of = __shfl_xor(f, off, 64);
+    m = om > m ? om : m;
+    f |= of;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    rm[threadIdx.x >> 6] = m;
+    rf[threadIdx.x >> 6] = f;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+      m = rm[w] > m ? rm[w] : m;
+      f |= rf[w];
+    }
+    __hip_atomic_store(pub, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(pub + 1, f ? 1ULL : 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// a workgroup's contribution in the deferred form
+__device__ __forceinline__ void eps_store_part(unsigned long long* part, double bm, int bnf)
+{
+  part[2 * blockIdx.x] = bm > 0.0 ? (unsigned long long)__double_as_longlong(bm) : 0ULL;   // NaN never wins
+  part[2 * blockIdx.x + 1] = bnf ? 1ULL : 0ULL;
+}
+
+__global__ __launch_bounds__(256) void eps_reduce_kernel(const unsigned long long* part, int n,
+                                                         unsigned long long* pub)
+{
+  eps_reduce_publish(part, n, pub);
 }
 
 
@@ -560,6 +615,11 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
   const int WX = a.gwx, TY = a.gty, TX = 2 * WX, LW = TX + 4, LH = TY + 2, NH = LW + 2 * TY;
   __shared__ __attribute__((aligned(16))) double lds[2][3][PFT_FUSED_LF];
 
+  if (STAGE == 1 && a.npart > 0 && (int)blockIdx.x == a.ntile * a.nchunk) {
+    // the extra workgroup of a speculative stage 1: the previous launch's error norm
+    eps_reduce_publish(a.part, a.npart, a.pub);
+    return;
+  }
   const int ntx = (a.n1 + TX - 1) / TX;
   const int lin = xcd_remap(blockIdx.x, a.ntile * a.nchunk);
   const int tile = lin % a.ntile, chunk = lin / a.ntile;
@@ -620,28 +680,26 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
   int cur = 0;
   if (kb < ke) {
     const long o0 = (long)(kb + 1) * a.plane + po;
+    const bool wlo = kb == 0 && !a.has_below;
+    const long ob = wlo ? o0 : o0 - a.plane;
+    Ops cop[3], bop[3], hop;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) load_ops<STAGE, GLS>(a, q, o0, cop[q]);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) load_ops<STAGE, GLS>(a, q, ob, bop[q]);
+    load_ops<STAGE, GLS>(a, hf, (long)(kb + 1) * a.plane + hp, hop);
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
-      Ops cop;
-      load_ops<STAGE, GLS>(a, q, o0, cop);
-      zc[q] = stage_in<STAGE, GLS>(a, q, cop);
-      if constexpr (SUM2) s2c[q] = cop.k1;
-      if (STAGE == 5) keep5<GLS>(q, cop, cx[q], ck1[q], ck4[q], cE[q]);
-      if (kb == 0 && !a.has_below) {
-        zm[q] = zc[q];                                  // bottom wall mirror (equation.c:164-174)
-      } else {
-        Ops tmp;
-        load_ops<STAGE, GLS>(a, q, o0 - a.plane, tmp);  // plane below (exchanged ghost at kb == 0)
-        zm[q] = stage_in<STAGE, GLS>(a, q, tmp);
-      }
+      zc[q] = stage_in<STAGE, GLS>(a, q, cop[q]);
+      if constexpr (SUM2) s2c[q] = cop[q].k1;
+      if (STAGE == 5) keep5<GLS>(q, cop[q], cx[q], ck1[q], ck4[q], cE[q]);
+      zm[q] = wlo ? zc[q] : stage_in<STAGE, GLS>(a, q, bop[q]);
       st2x(&lds[0][q][lo], zc[q], c0);
     }
-    if (hact) {
-      Ops tmp;
-      load_ops<STAGE, GLS>(a, hf, (long)(kb + 1) * a.plane + hp, tmp);
-      const dbl2 v = stage_in<STAGE, GLS>(a, hf, tmp);
-      st2x(&lds[0][hf][hl], v, h0);
-    }
+    if (hact) st2x(&lds[0][hf][hl], stage_in<STAGE, GLS>(a, hf, hop), h0);
+    // the DEEP look-ahead after those loads are consumed, as before: the loop then starts with
+    // only the look-ahead in flight (with it issued together with the rest, the compiler's wait
+    // placement serialised the loop's own look-ahead: stage 1 at 400^3 0.149 -> 0.175 ms)
     if constexpr (DEEP) {
       if (!((kb == a.n3 - 1) && !a.has_above)) {
 #pragma unroll
@@ -802,7 +860,8 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
         if (red[q] > bm) bm = red[q];
         bnf |= rnf[q];
       }
-      eps_arrive(bm, bnf, a.shards, a.eps_bits, a.nonfinite, a.pub, a.pub_count);
+      if (a.part) eps_store_part(a.part, bm, bnf);
+      else eps_arrive(bm, bnf, a.shards, a.eps_bits, a.nonfinite, a.pub, a.pub_count);
     }
   }
 }
@@ -854,6 +913,7 @@ struct PairArgs {
   unsigned long long* pub;   // in-kernel publication of the error norm (as merson_fused<5>)
   unsigned int* pub_count;
   EpsShard* shards;    // the error norm's per-shard accumulators (eps_arrive)
+  unsigned long long* part;   // deferred publication: this launch's workgroup partials (eps_store_part)
   long fs;
   int n1, n2, n3, plane;
   int has_below, has_above;   // z-neighbours: stage A also runs on the ghost plane next to each,
@@ -1271,7 +1331,8 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
       // gl's error-norm term: the same constant at every cell (its K's are literal zeros)
       if (a.evgl > bm) bm = a.evgl;
       bnf |= !isfinite(a.evgl);
-      eps_arrive(bm, bnf, a.shards, a.eps_bits, a.nonfinite, a.pub, a.pub_count);
+      if (a.part) eps_store_part(a.part, bm, bnf);
+      else eps_arrive(bm, bnf, a.shards, a.eps_bits, a.nonfinite, a.pub, a.pub_count);
     }
   }
 }
@@ -1492,6 +1553,15 @@ struct pft_slab {
   unsigned long long* pub_ring_dev;  // its device address
   unsigned int* pub_count;           // device: finished workgroups of the publishing launch
   EpsShard* eps_shards;              // device: the error norm's shards (after pub_count's line)
+  unsigned long long* part;          // device: deferred publication partials (2 words per workgroup)
+  long part_cap;                     // ... their capacity in workgroups
+  int defer_n;                       // workgroups of the armed error-norm launch awaiting reduction
+  int defer_slot;                    // ... and its host slot
+  // host-side memos (a small slab is host-bound: ~5 launches of a few us per attempted step)
+  int fgeo_valid, fgeo_wx, fgeo_ty;  // fused_geometry(n1, n2) of this slab
+  double fgeo_eff;
+  long kz_key[16];                   // z-chunk cost model: key (occupancy, tiles, planes) -> kz
+  int kz_val[16];
   long pub_next;                     // slots used so far
   int pub_armed;                     // the last stage-5 launch publishes into slot pub_slot
   int pub_slot;
@@ -1691,6 +1761,7 @@ int pft_slab_destroy(pft_slab* s)
   if (s->host_pub) (void)hipHostFree(s->host_pub);
   if (s->pub_ring) (void)hipHostFree(s->pub_ring);
   if (s->pub_count) (void)hipFree(s->pub_count);
+  if (s->part) (void)hipFree(s->part);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   if (s->comm) (void)hipStreamDestroy(s->comm);
   if (s->side) (void)hipStreamDestroy(s->side);
@@ -1881,6 +1952,59 @@ static double fused_geometry(int n1, int n2, int* wx_out, int* ty_out)
   return best;   // busy lanes / launched lanes over the plane
 }
 
+// fused_geometry of the slab's plane, computed once (slab_kind and every launch ask for it)
+static double slab_fgeo(const pft_slab* cs, int* wx, int* ty)
+{
+  pft_slab* s = const_cast<pft_slab*>(cs);
+  if (!s->fgeo_valid) {
+    s->fgeo_eff = fused_geometry(s->d.n1, s->d.n2, &s->fgeo_wx, &s->fgeo_ty);
+    s->fgeo_valid = 1;
+  }
+  *wx = s->fgeo_wx;
+  *ty = s->fgeo_ty;
+  return s->fgeo_eff;
+}
+
+// z-chunk count memo: the cost models below scan every chunk count (400 planes: 400 candidates);
+// their result only depends on the occupancy, the tile count and the planes
+static int kz_memo_get(const pft_slab* s, int slot, long key)
+{
+  return s->kz_key[slot] == key + 1 ? s->kz_val[slot] : 0;
+}
+static void kz_memo_put(pft_slab* s, int slot, long key, int kz)
+{
+  s->kz_key[slot] = key + 1;
+  s->kz_val[slot] = kz;
+}
+
+// planes per z-chunk: a CU runs `occ` workgroups at a time; a chunk count with w = ceil(workgroups /
+// CUs) workgroups per CU costs (planes per chunk + the two planes a chunk re-reads) times
+//   - occ <= 2: ceil(w / occ) rounds -- a partial last round runs a CU at half its waves and the
+//     HBM-bound stages stall;
+//   - occ >= 3: max(1, w / occ) -- retiring workgroups are refilled at once, and the extra
+//     workgroups help the arithmetic-heavy stages hide latency.
+// The cheapest count wins (more chunks only when 5% cheaper).
+static int chunk_kz(pft_slab* s, int slot, int occ, long ntile, int nplanes)
+{
+  const long key = ((long)occ << 52) ^ (ntile << 24) ^ (long)nplanes;
+  int kz = kz_memo_get(s, slot, key);
+  if (kz) return kz;
+  int best_nch = 1;
+  double best_cost = -1.0;
+  for (int nch = 1; nch <= nplanes; ++nch) {
+    const int k = (nplanes + nch - 1) / nch;
+    if (nch > 1 && k == (nplanes + nch - 2) / (nch - 1)) continue;   // same kz as nch - 1
+    const long nb = ntile * ((nplanes + k - 1) / k);
+    const long per_cu = (nb + s->n_cu - 1) / s->n_cu;
+    const double rounds = occ <= 2 ? (double)((per_cu + occ - 1) / occ) : std::max(1.0, (double)per_cu / occ);
+    const double cost = rounds * (k + 2);
+    if (best_cost < 0.0 || cost < 0.95 * best_cost) { best_cost = cost; best_nch = nch; }
+  }
+  kz = (nplanes + best_nch - 1) / best_nch;
+  kz_memo_put(s, slot, key, kz);
+  return kz;
+}
+
 static int slab_kind(const pft_slab* s)
 {
   // 16-byte rows need n1 even; the aux-array path (recompute off) is the cache kernel's.  (An
@@ -1893,7 +2017,7 @@ static int slab_kind(const pft_slab* s)
   // Mcells*steps/s (47 vs 60 us per attempted step untimed)
   if (s->tile_wx == 1) {
     int wx, ty;
-    if (fused_geometry(s->d.n1, s->d.n2, &wx, &ty) < 0.7) return KCACHE;
+    if (slab_fgeo(s, &wx, &ty) < 0.7) return KCACHE;
   }
   return KFUSED;
 }
@@ -1915,7 +2039,7 @@ int pft_slab_tile_geometry(const pft_slab* s, int stage, int* wx, int* ty)
     *wx = 0;
     *ty = 0;
   } else if (kind == KFUSED && auto_tile) {
-    fused_geometry(s->d.n1, s->d.n2, wx, ty);
+    slab_fgeo(s, wx, ty);
   } else {
     *wx = s->tile_wx;
     *ty = PFT_FBLOCK / *wx;
@@ -1934,6 +2058,24 @@ int pft_slab_stage_fields(const pft_slab* s, int stage)
   // neighbours' XN gl ghost planes already equal X's (both exchanged at upload)
   if (stage == 5 && pft_slab_get_gl_keep(s) && slab_kind(s) == KFUSED) return 2;
   return 3;
+}
+
+// arm the deferred publication of an error-norm launch of nwg workgroups into host slot j: its
+// workgroups store partials (eps_store_part), the next stage-1 launch reduces and publishes them
+static int defer_arm(pft_slab* s, long nwg, int j, unsigned long long** part)
+{
+  if (nwg > s->part_cap) {
+    if (s->part) HIPCHK(hipFree(s->part));
+    s->part = nullptr;
+    s->part_cap = 0;
+    const long cap = std::max(nwg, 4096L);
+    HIPCHK(hipMalloc((void**)&s->part, 16 * (size_t)cap));
+    s->part_cap = cap;
+  }
+  s->defer_n = (int)nwg;
+  s->defer_slot = j;
+  *part = s->part;
+  return 0;
 }
 
 static int run_stage(pft_slab* s, int stage, const double* in, double* kout, double* out, double t_stage,
@@ -1981,7 +2123,7 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   const int wx = kind == KCACHE ? 0 : auto_tile ? (stage <= 2 ? 16 : 32) : s->tile_wx;
   if (kind == KFUSED) {
     if (auto_tile) {
-      fused_geometry(s->d.n1, s->d.n2, &a.gwx, &a.gty);
+      slab_fgeo(s, &a.gwx, &a.gty);
     } else {
       a.gwx = s->tile_wx;
       a.gty = PFT_FBLOCK / s->tile_wx;
@@ -1998,30 +2140,14 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   if (s->kz > 0) {
     a.kz = s->kz;
   } else {
-    // automatic: a CU runs `occ` workgroups at a time; a chunk count with w = ceil(workgroups /
-    // CUs) workgroups per CU costs (planes per chunk + the two planes a chunk re-reads) times
-    //   - occ <= 2: ceil(w / occ) rounds -- a partial last round runs a CU at half its waves and
-    //     the HBM-bound stages stall;
-    //   - occ >= 3: max(1, w / occ) -- retiring workgroups are refilled at once, and the extra
-    //     workgroups help the arithmetic-heavy stages hide latency.
-    // The cheapest count wins (more chunks only when 5% cheaper).  Measured at 400^3 (80 tiles):
+    // automatic (chunk_kz)
+    // Measured at 400^3 (80 tiles):
     // stage 5 (occ 2) 6 chunks, 0.348 ms vs 0.393 for 16; stage 1 (occ 3) 16 chunks of 25 planes,
     // 0.153 vs 0.163 for 9 of 45.  On a 400 x 400 x 100 slab (320 tiles, one 800^3 8-way rank)
     // stages 4-5: 3 chunks (960 workgroups, 2 rounds) 0.261 / 0.349 ms against 0.314 / 0.436 for
     // one round of 320 (64 CUs with 2 workgroups, 192 with 1).
     const int occ = stage_occupancy(stage, mode, gls, kind, wx);
-    int best_nch = 1;
-    double best_cost = -1.0;
-    for (int nch = 1; nch <= nplanes; ++nch) {
-      const int kz = (nplanes + nch - 1) / nch;
-      if (nch > 1 && kz == (nplanes + nch - 2) / (nch - 1)) continue;   // same kz as nch - 1
-      const long nb = (long)a.ntile * ((nplanes + kz - 1) / kz);
-      const long per_cu = (nb + s->n_cu - 1) / s->n_cu;
-      const double rounds = occ <= 2 ? (double)((per_cu + occ - 1) / occ) : std::max(1.0, (double)per_cu / occ);
-      const double cost = rounds * (kz + 2);
-      if (best_cost < 0.0 || cost < 0.95 * best_cost) { best_cost = cost; best_nch = nch; }
-    }
-    a.kz = (nplanes + best_nch - 1) / best_nch;
+    a.kz = chunk_kz(s, stage + 6 * (gls ? 1 : 0), occ, a.ntile, nplanes);
   }
   a.nchunk = (nplanes + a.kz - 1) / a.kz;
   a.kspan = a.kz;
@@ -2050,12 +2176,20 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
     const int j = (int)(s->pub_next % PFT_PUB_SLOTS);
     __atomic_store_n(&s->pub_ring[2 * j], PFT_PUB_SENTINEL, __ATOMIC_RELEASE);
     __atomic_store_n(&s->pub_ring[2 * j + 1], PFT_PUB_SENTINEL, __ATOMIC_RELEASE);
-    a.pub = s->pub_ring_dev + 2 * j;
-    a.pub_count = s->pub_count;
+    const int rc = defer_arm(s, (long)a.ntile * a.nchunk, j, &a.part);
+    if (rc) return rc;
     s->pub_armed = 1;
     s->pub_slot = j;
   }
   dim3 g((unsigned)(a.ntile * a.nchunk));
+  if (stage == 1 && kind == KFUSED && s->defer_n > 0) {
+    // the previous error-norm launch's partials: reduced and published by one extra workgroup
+    a.part = s->part;
+    a.npart = s->defer_n;
+    a.pub = s->pub_ring_dev + 2 * s->defer_slot;
+    s->defer_n = 0;
+    g.x += 1;
+  }
   const hipStream_t st = s->stream;
   if (gls)
     launch_stage<true>(stage, mode, kind, wx, g, st, a, s->c);
@@ -2151,6 +2285,7 @@ int pft_slab_set_inkernel_publish(pft_slab* s, int on)
 {
   s->inkernel_pub = on ? 1 : 0;
   s->pub_armed = 0;
+  s->defer_n = 0;
   return 0;
 }
 
@@ -2177,9 +2312,15 @@ int pft_slab_eps_mark_on(pft_slab* s, void* stream)
 int pft_slab_eps_fetch(pft_slab* s, double* eps, int* nonfinite)
 {
   if (s->eps_marked == 2) {
-    // published by the stage-5 kernel: poll the slot (pinned, coherent) until both words left the
-    // sentinel; the speculative stage 1 behind it keeps running
+    // published beside the speculative stage 1 (deferred publication): poll the slot (pinned,
+    // coherent) until both words left the sentinel while that kernel keeps running.  Without a
+    // stage-1 launch since the error-norm launch, a one-workgroup reduction publishes instead.
     s->eps_marked = 0;
+    if (s->defer_n > 0) {
+      eps_reduce_kernel<<<1, 256, 0, s->stream>>>(s->part, s->defer_n, s->pub_ring_dev + 2 * s->defer_slot);
+      s->defer_n = 0;
+      HIPCHK(hipGetLastError());
+    }
     volatile unsigned long long* w = s->pub_ring + 2 * s->pub_slot;
     long spins = 0;
     double t0 = 0.0;
@@ -2428,18 +2569,7 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
     // z-chunks as run_stage's cost model: a chunk of kz planes evaluates stage A on kz + 2 and
     // loads kz + 3; `occ` workgroups per CU (one: 141 KiB of LDS)
     const int occ = first == 2 ? pair_occupancy_mode<2, false>(mode) : pair_occupancy_mode<4, false>(mode);
-    int best_nch = 1;
-    double best_cost = -1.0;
-    for (int nch = 1; nch <= nplanes; ++nch) {
-      const int kz = (nplanes + nch - 1) / nch;
-      if (nch > 1 && kz == (nplanes + nch - 2) / (nch - 1)) continue;
-      const long nb = (long)a.ntile * ((nplanes + kz - 1) / kz);
-      const long per_cu = (nb + s->n_cu - 1) / s->n_cu;
-      const double rounds = occ <= 2 ? (double)((per_cu + occ - 1) / occ) : std::max(1.0, (double)per_cu / occ);
-      const double cost = rounds * (kz + 2);
-      if (best_cost < 0.0 || cost < 0.95 * best_cost) { best_cost = cost; best_nch = nch; }
-    }
-    a.kz = (nplanes + best_nch - 1) / best_nch;
+    a.kz = chunk_kz(s, 12 + (first == 4 ? 1 : 0), occ, a.ntile, nplanes);
   }
   a.nchunk = (nplanes + a.kz - 1) / a.kz;
   a.kspan = a.kz;
@@ -2467,8 +2597,8 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
     const int j = (int)(s->pub_next % PFT_PUB_SLOTS);
     __atomic_store_n(&s->pub_ring[2 * j], PFT_PUB_SENTINEL, __ATOMIC_RELEASE);
     __atomic_store_n(&s->pub_ring[2 * j + 1], PFT_PUB_SENTINEL, __ATOMIC_RELEASE);
-    a.pub = s->pub_ring_dev + 2 * j;
-    a.pub_count = s->pub_count;
+    const int rc = defer_arm(s, (long)a.ntile * a.nchunk, j, &a.part);
+    if (rc) return rc;
     s->pub_armed = 1;
     s->pub_slot = j;
   }

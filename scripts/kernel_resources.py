@@ -10,7 +10,7 @@ import sys
 flt = re.compile(sys.argv[1] if len(sys.argv) > 1 else "merson_fused")
 extra = sys.argv[2:]
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=off",
-       "-fno-fast-math", "-Wno-unused-result", "-c", "porousfreezethaw_amd/csrc/pft_kernels.hip", "-o",
+       "-fno-fast-math", "-Wno-unused-result", "-c", __import__("os").environ.get("PFT_SRC","porousfreezethaw_amd/csrc/pft_kernels.hip"), "-o",
        "/tmp/pft_kernels_res.o", "-Rpass-analysis=kernel-resource-usage"] + extra
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 rows, cur = [], None
