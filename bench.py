@@ -239,7 +239,8 @@ def main():
         if os.path.exists(pmc):
             try:
                 ps = json.load(open(pmc))
-                key = f"{'pair' if pairs else 'stage'}{dom}_gl{int(a.gl_static)}_{n1}x{n2}x{sim.grid.n3}_m{a.mode}"
+                gk = f"glx{int(a.gl_static or gl_keep)}" if pairs else f"gl{int(a.gl_static)}"
+                key = f"{'pair' if pairs else 'stage'}{dom}_{gk}_{n1}x{n2}x{sim.grid.n3}_m{a.mode}"
                 traffic = ps.get(key, {}).get("hbm_bytes_per_launch")
                 valu_frac = ps.get(key, {}).get("valu_issue_frac")
                 f64 = {q: ps.get(key, {}).get(q) for q in ("fp64_flop_per_launch", "fp64_pipe_busy_frac")}
@@ -251,7 +252,7 @@ def main():
                 traffic = None
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": kernel_name(dom, a, rc_path, n1, pairs),
+                "kernel": kernel_name(dom, a, rc_path, n1, pairs, gl_keep),
                 # the pair kernels are FP64-VALU-bound (stage A recomputed on a ring, no HBM bytes
                 # spared to compute): the fraction of the SIMDs' issue cycles their VALU
                 # instructions take, from the same PMC file (SQ_INSTS_VALU, GRBM_GUI_ACTIVE)
@@ -454,17 +455,15 @@ def workload(grid_nodes, world, shape="cube", literal_cube=False, mode=0, domain
             (base["L1"], base["L2"], base["L3"] * world))
 
 
-def kernel_name(stage, a, rc_path, n1, pairs=False):
-    """the stage kernel libpft launches for these options (pft_kernels.hip launch_stage, run_pair)"""
+def kernel_name(stage, a, rc_path, n1, pairs=False, glx=False):
+    """the stage kernel libpft launches for these options (pft_kernels.hip launch_stage, run_pair);
+    a pair kernel's third parameter is GLX (gl's inputs read from x: gl_static, or gl_keep)"""
     gls = "true" if a.gl_static else "false"
     if pairs and stage in (3, 5):
-        return f"merson_pair<{stage - 1}, {a.mode}, {gls}>"
-    if a.tile == 0 or n1 % 2:
+        return f"merson_pair<{stage - 1}, {a.mode}, {'true' if (a.gl_static or glx) else 'false'}>"
+    if a.tile == 0 or n1 % 2 or not rc_path:
         return f"merson_stage<{stage}, {a.mode}, {gls}>"
-    wx = (16 if stage <= 2 else 32) if a.tile == 1 else a.tile
-    if rc_path:
-        return f"merson_fused<{stage}, {a.mode}, {gls}>"
-    return f"merson_tile<{stage}, {a.mode}, {gls}, {wx}>"
+    return f"merson_fused<{stage}, {a.mode}, {gls}>"
 
 
 def cpu_baseline(sim, base, a):

@@ -8,7 +8,7 @@
 # Every GPU step runs under its own time limit; a crash/fault/timeout ends the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
-TAG=${TAG:-r02}
+TAG=${TAG:-r03}
 export TAG PMC_DATE=${PMC_DATE:-$(date -u +%F)} PMC_GIT=${PMC_GIT:-unknown}
 O=gpurun_out/ev
 mkdir -p $O/prof
@@ -47,4 +47,12 @@ for dom in "400 0.06,0.06,0.015 n8" "318 0.06,0.06,0.03 n4" "252 0.06,0.06,0.06 
     timeout -k 10 300 python bench.py --steps 100 --no-cpu --grid-nodes $1 --domain $2 --self-exchange --transport $tr > $O/bench_slab_$3_selfx_$tr.json 2>> $O/bench_var.err; fatal $? slab_$3_selfx_$tr
   done
 done
+# the driver's own configuration (--steps 20 --warmup 5) three times, and its per-launch kernel trace
+# (the clock transient after the warm-up)
+for r in 1 2 3; do
+  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu > $O/bench_driver_$r.json 2>> $O/bench_var.err; fatal $? bench_driver
+done
+timeout -k 10 300 rocprofv3 --kernel-trace -d $O/prof/driver -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu > $O/prof/driver_bench.json 2> $O/prof/driver.err; fatal $? driver_trace
+# bench.py --gpus N rehearsed on this one GPU (ipc ranks) with its decomposition parity check
+bash scripts/bench_multi.sh > $O/bench_multi.log 2>&1; fatal $? bench_multi
 echo done >> $O/status.log

@@ -77,7 +77,8 @@ def main(trace_dir, fetch_dir, write_dir, dims, probe_bytes, out_path, valu_dir=
             continue
         fb = fetch.get(k, 0.0) * 1024 * cal_f
         wb = write.get(k, 0.0) * 1024 * cal_w
-        key = f"{st}_gl{int(gls)}_{dims}_m{mode}"
+        # a pair kernel's third template parameter is GLX (gl_static or gl_keep), a stage kernel's GLS
+        key = f"{st}_{'glx' if st.startswith('pair') else 'gl'}{int(gls)}_{dims}_m{mode}"
         res[key] = {"kernel": k, "fetch_bytes": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb,
                     "raw_FETCH_SIZE_KiB": fetch.get(k), "raw_WRITE_SIZE_KiB": write.get(k)}
         if k in valu and grbm.get(k):
