@@ -157,6 +157,29 @@ int pft_slab_swap_buffers(pft_slab * s, int a, int b);
 int pft_slab_can_speculate(const pft_slab * s);
 int pft_slab_stage_spec(pft_slab * s, double t_stage, int k_begin, int k_end);
 int pft_slab_eps_mark(pft_slab * s);
+/* Gated steps (f4, one slab, fused stage launches): the launches of the next attempted step are
+   enqueued BEFORE this step's error norm is known, so that the GPU waits neither for the host's
+   decision nor for its launch latency between steps.  They assume the step is accepted (the caller
+   swaps the buffers as pft_slab_accept would for the enqueue, and back) and run on the DEVICE's
+   decision: the speculative stage 1 of this step, once it has reduced the error norm, decides the
+   step as hybrid2.c:578-611 does (pow from ocml) and writes the next step's t and h, or a skip.
+   The host takes its own decision (glibc pow) and keeps the gated step only if both agree bit for
+   bit; otherwise it discards it (its outputs are never read) and launches the step again.
+     gate_config(final_time, delta, h_min, delta_local, handle_nan)  the solve's constants
+     gate_arm(t, h)      the next speculative stage-1 launch decides step (t, h) (ignored when that
+                         launch is gated itself: it decides its own step); returns the decision seq
+     gate_use(seq | 0)   launches enqueued from now on run only if decision seq accepted the step
+     gate_decision(seq, &go, &t, &h)  the device's decision (waits for its publication)
+   book_save/load(0|1): the error-norm publication bookkeeping, so that this step's error norm is
+   fetched after the next step's launches were enqueued (save 0, enqueue, save 1, load 0, fetch;
+   on a kept gated step load 1). */
+int pft_slab_gate_config(pft_slab * s, double final_time, double delta, double h_min, int delta_local,
+                         int handle_nan);
+unsigned long long pft_slab_gate_arm(pft_slab * s, double t, double h);
+int pft_slab_gate_use(pft_slab * s, unsigned long long seq);
+int pft_slab_gate_decision(pft_slab * s, unsigned long long seq, int * go, double * t, double * h);
+int pft_slab_book_save(pft_slab * s, int which);
+int pft_slab_book_load(pft_slab * s, int which);
 /* Pair kernels (one slab, recompute path): stages 2+3 or 4+5 of the step (first = 2 or 4) in ONE
    launch.  Stage A's K is evaluated on the tile and a one-cell ring and never stored; stage B
    writes K3 (first = 2) or the error norm and x(t+h) into XN (first = 4), bit for bit what the

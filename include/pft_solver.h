@@ -64,9 +64,14 @@ enum {
 	                           16 Ki cells per CU (4 M cells on MI355X), 2 = on any slab they fit,
 	                           0 = one launch per stage */
 	,
-	PFT_OPT_FAIL_RHS = 11   /* test hook: N > 0 makes the N-th device evaluation of libpft's own
+	PFT_OPT_FAIL_RHS = 11,  /* test hook: N > 0 makes the N-th device evaluation of libpft's own
 	                           right-hand side on a host array (f_generic_model01/2 called by the
 	                           host-staged path) fail as a device fault would; 0 (default) off */
+	PFT_OPT_GATE = 12       /* gated steps (f4): 1 (default) = on one slab with one launch per
+	                           stage and no Service_Callback, the next attempted step's launches are
+	                           enqueued before this step's error norm is read and run on the
+	                           device's step decision, which the host checks bit for bit
+	                           (pft_slab_gate_*); 0 = off.  Bit-identical either way. */
 };
 int pft_solver_set_option(int opt, long value);
 
@@ -80,6 +85,10 @@ typedef struct {
 	long stage_n[6];        /* number of timed stage executions */
 	int pairs;              /* 1: the last fused call ran stages 2+3 and 4+5 as pair kernels
 	                           (timed as stages 3 and 5) */
+	long gated_steps;       /* attempted steps of the last call that ran as pre-enqueued gated
+	                           launches (PFT_OPT_GATE) */
+	long gate_misses;       /* ... that were discarded because the device's step size differed
+	                           from the host's in the last bit (pow) and were launched again */
 } pft_solver_stats;
 int pft_solver_get_stats(pft_solver_stats * st);
 

@@ -30,6 +30,7 @@ PFT_SOLVE_KEEP_DEVICE, PFT_SOLVE_REUSE_DEVICE = 1, 2
 PFT_OPT_GL_STATIC, PFT_OPT_KZ, PFT_OPT_DEVICE, PFT_OPT_TIMING, PFT_OPT_TILE, PFT_OPT_RECOMPUTE = 1, 2, 3, 4, 5, 6
 PFT_OPT_LAZY_ALLOC = 9
 PFT_OPT_PAIR = 10
+PFT_OPT_GATE = 12
 PFT_OPT_FAIL_RHS = 11
 PFT_SOLVE_DEVICE_ERROR = -7
 MPI_COMM_WORLD = 0x44000000
@@ -79,7 +80,8 @@ class pft_snapshot_info(C.Structure):
 class pft_solver_stats(C.Structure):
     _fields_ = [("path", C.c_int), ("nprocs", C.c_int), ("rank", C.c_int),
                 ("kernel_launches", C.c_long), ("steps_total", C.c_long), ("last_eps", C.c_double),
-                ("stage_ms", C.c_double * 6), ("stage_n", C.c_long * 6), ("pairs", C.c_int)]
+                ("stage_ms", C.c_double * 6), ("stage_n", C.c_long * 6), ("pairs", C.c_int),
+                ("gated_steps", C.c_long), ("gate_misses", C.c_long)]
 
 
 _lib = None

@@ -232,7 +232,82 @@ struct StageArgs {
   // stage 1 with npart > 0 reduces npart partials in its last workgroup and publishes them to pub
   unsigned long long* part;
   int npart;
+  // Gated step (f4, small slabs, pft_slab_gate_*): this launch was enqueued before the step it
+  // belongs to was decided.  gate -> 3 device words the previous speculative stage 1 wrote with
+  // its decision (gate_decide): [0] a sequence number (the launch runs iff == gseq; the skip bit
+  // never equals it), [1] t, [2] h of the step (bit patterns): the launch derives its scalars
+  // from them with the solver's own expressions (gate_scalars).
+  const unsigned long long* gate;
+  unsigned long long gseq;
+  // ... and the decision: the speculative stage 1's extra workgroup, once it has the error norm,
+  // decides the step as hybrid2.c:578-611 does and writes it to gdev (for the launches gated on
+  // it) and to pinned gpin (for the host, which takes its own decision and compares bit for bit).
+  // gdec_seq: its sequence number; dt, dh: t and h of the step being decided (a gated launch
+  // takes them from its gate); the solve's constants: final time, delta, h_min, delta_mode ==
+  // DELTA_LOCAL, handle_nan.
+  unsigned long long* gdev;
+  unsigned long long* gpin;
+  unsigned long long gdec_seq;
+  double dt, dh, d_final, d_delta, d_hmin;
+  int d_local, d_nan;
 };
+
+#define PFT_GATE_SKIP (1ULL << 63)
+#define PFT_GATE_SLOTS 64
+
+// the scalars of a gated launch from the decided (t, h), exactly as rk_solver.c's run_fused and
+// run_stage form them (hybrid2.c:355: h/2.0, h/3.0, h/6.0, h/8.0; the stage times t + h3, t + h2,
+// t + h; equation.c:110 T_top; the stage-input coefficients h/3.0, h/6.0, h/8.0, h).  IEEE
+// division and addition are correctly rounded on both sides (-ffp-contract=off): the same bits.
+template <int STAGE>
+__device__ __forceinline__ void gate_scalars(StageArgs& a, const pft_consts& c, double t, double h)
+{
+  const double h2 = h / 2.0, h3 = h / 3.0, h6 = h / 6.0, h8 = h / 8.0;
+  double ts = t + h;
+  if (STAGE == 1) {                      // the speculative stage 1 of the next step (coef 0, h 0)
+    a.coef = 0.0;
+    a.h = h;
+    a.cin = h;
+  } else {
+    ts = STAGE <= 3 ? t + h3 : (STAGE == 4 ? t + h2 : t + h);
+    a.coef = STAGE == 2 ? h6 : (STAGE == 3 ? h8 : (STAGE == 4 ? h : h3));
+    a.h = h;
+    a.cin = STAGE == 2 ? h / 3.0 : (STAGE == 3 ? h / 6.0 : (STAGE == 4 ? h / 8.0 : h));
+  }
+  a.T_top = ts < c.phase_switch_time ? c.top_temp1 : c.top_temp2;
+  if (STAGE == 5) a.gl_keep = a.gl_keep && isfinite(a.coef);
+}
+
+// One thread: the step-size control of hybrid2.c:578-611 (rk_solver.c run_fused_impl restates it
+// on the host) for the step (t, h) whose error norm bits epsb / non-finite flag nf were just
+// reduced: the next step's (t, h) when it is accepted, a skip when it is rejected or hit a NaN.
+// The only operation not correctly rounded is pow (ocml here, glibc on the host): the host takes
+// its own decision and runs the gated step only if both agree bit for bit (otherwise it discards
+// it and launches the step again with its own h).
+__device__ __forceinline__ void gate_decide(const StageArgs& a, double t, double h, unsigned long long epsb, int nf,
+                                            bool have_eps)
+{
+  double eps = __longlong_as_double((long long)epsb);
+  unsigned long long v = a.gdec_seq | PFT_GATE_SKIP, tb = 0, hb = 0;
+  if (have_eps && !(a.d_nan && nf)) {                                      // :493-503
+    const double h3 = h / 3.0;
+    if (a.d_local) eps *= fabs(h3);                                        // :578
+    const double new_h = ((eps > 0.0) ? pow((a.d_delta / eps), 0.2) * 0.8 : 2.0) * h;   // :580
+    if (eps < a.d_delta || fabs(h) < a.d_hmin) {                           // :599-611
+      const double tn = t + h;                                             // :652
+      const double hn = (fabs(a.d_final - tn) <= fabs(new_h)) ? a.d_final - tn : new_h;   // :743-761
+      tb = (unsigned long long)__double_as_longlong(tn);
+      hb = (unsigned long long)__double_as_longlong(hn);
+      v = a.gdec_seq;
+    }
+  }
+  a.gdev[1] = tb;
+  a.gdev[2] = hb;
+  __hip_atomic_store(a.gdev, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(a.gpin + 1, tb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(a.gpin + 2, hb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(a.gpin, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // a value the error norm never takes (a NaN pattern: the max skips NaN) nor the flag
 #define PFT_PUB_SENTINEL 0xFFF8DEADBEEF0001ULL
@@ -291,7 +366,8 @@ __device__ __forceinline__ void eps_arrive(double bm, int bnf, EpsShard* shards,
 // workgroups spent ~1-2 us in the arrival atomics), and the kernel boundary orders the plain stores
 // before the reads.  One block of 256 threads; called with the block's threads.
 __device__ __forceinline__ void eps_reduce_publish(const unsigned long long* __restrict__ part, int n,
-                                                   unsigned long long* pub)
+                                                   unsigned long long* pub, unsigned long long* mo = nullptr,
+                                                   unsigned long long* fo = nullptr)
 {
   __shared__ unsigned long long rm[4], rf[4];
   unsigned long long m = 0, f = 0;
@@ -318,6 +394,8 @@ __device__ __forceinline__ void eps_reduce_publish(const unsigned long long* __r
     }
     __hip_atomic_store(pub, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(pub + 1, f ? 1ULL : 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (mo) *mo = m;
+    if (fo) *fo = f;
   }
 }
 
@@ -615,9 +693,22 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
   const int WX = a.gwx, TY = a.gty, TX = 2 * WX, LW = TX + 4, LH = TY + 2, NH = LW + 2 * TY;
   __shared__ __attribute__((aligned(16))) double lds[2][3][PFT_FUSED_LF];
 
-  if (STAGE == 1 && a.npart > 0 && (int)blockIdx.x == a.ntile * a.nchunk) {
-    // the extra workgroup of a speculative stage 1: the previous launch's error norm
-    eps_reduce_publish(a.part, a.npart, a.pub);
+  if (a.gate) {
+    // a gated launch: run iff the step it belongs to was accepted (t, h from the decision), else
+    // leave before any store
+    const unsigned long long gs = __hip_atomic_load(a.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (gs != a.gseq) return;
+    const double gt = __longlong_as_double((long long)a.gate[1]), gh = __longlong_as_double((long long)a.gate[2]);
+    gate_scalars<STAGE>(a, c, gt, gh);
+    a.dt = gt;
+    a.dh = gh;
+  }
+  if (STAGE == 1 && (a.npart > 0 || a.gdev) && (int)blockIdx.x == a.ntile * a.nchunk) {
+    // the extra workgroup of a speculative stage 1: the previous launch's error norm, then (gated
+    // steps) the decision on the step it ended
+    unsigned long long m = 0, f = 0;
+    if (a.npart > 0) eps_reduce_publish(a.part, a.npart, a.pub, &m, &f);
+    if (a.gdev && threadIdx.x == 0) gate_decide(a, a.dt, a.dh, m, (int)f, a.npart > 0);
     return;
   }
   const int ntx = (a.n1 + TX - 1) / TX;
@@ -1565,6 +1656,24 @@ struct pft_slab {
   long pub_next;                     // slots used so far
   int pub_armed;                     // the last stage-5 launch publishes into slot pub_slot
   int pub_slot;
+  // gated steps (f4, pft_slab_gate_*): the host's decisions on the next step go to a ring of
+  // pinned slots (4 words: seq, t bits, h bits, pad); the speculative stage 1's extra workgroup
+  // copies its slot into the device ring, which the pre-enqueued launches of that step read
+  unsigned long long* gate_pin;      // host address, PFT_GATE_SLOTS x 4 words
+  unsigned long long* gate_pin_dev;  // its device address
+  unsigned long long* gate_dev;      // device ring, PFT_GATE_SLOTS x 4 words
+  unsigned long long gate_seq;       // the last sequence number handed out
+  unsigned long long gate_arm_seq;   // the next speculative stage-1 launch decides this step ...
+  double gate_arm_t, gate_arm_h;     // ... (t, h) of it (ignored when that launch is gated itself)
+  unsigned long long gate_use_seq;   // launches enqueued now are gated on this decision (0: not)
+  double gate_final, gate_delta, gate_hmin;   // the solve's constants (pft_slab_gate_config)
+  int gate_local, gate_nan;
+  // eps-publication bookkeeping snapshots (pft_slab_book_save/load): the launches of the next
+  // step are enqueued between this step's launches and the read of its error norm
+  struct Book {
+    long pub_next;
+    int pub_armed, pub_slot, eps_marked, defer_n, defer_slot;
+  } book[2];
   int kz;                // planes per workgroup z-march; 0 = automatic (z-chunk cost model)
   int n_cu;               // compute units of the slab's device
   double* noise;         // device u_noise (n3*plane) or null
@@ -1714,6 +1823,12 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
   if (e == hipSuccess)
     e = hipHostMalloc((void**)&s->pub_ring, 16 * PFT_PUB_SLOTS, hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&s->pub_ring_dev, s->pub_ring, 0);
+  if (e == hipSuccess)
+    e = hipHostMalloc((void**)&s->gate_pin, 32 * PFT_GATE_SLOTS, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&s->gate_pin_dev, s->gate_pin, 0);
+  if (e == hipSuccess) memset(s->gate_pin, 0, 32 * PFT_GATE_SLOTS);
+  if (e == hipSuccess) e = hipMalloc((void**)&s->gate_dev, 32 * PFT_GATE_SLOTS);
+  if (e == hipSuccess) e = hipMemsetAsync(s->gate_dev, 0, 32 * PFT_GATE_SLOTS, s->stream);
   const size_t cnt_bytes = 64 + sizeof(EpsShard) * PFT_EPS_SHARDS;
   if (e == hipSuccess) e = hipMalloc((void**)&s->pub_count, cnt_bytes);
   if (e == hipSuccess) e = hipMemsetAsync(s->pub_count, 0, cnt_bytes, s->stream);
@@ -1760,6 +1875,8 @@ int pft_slab_destroy(pft_slab* s)
   if (s->host_scratch) (void)hipHostFree(s->host_scratch);
   if (s->host_pub) (void)hipHostFree(s->host_pub);
   if (s->pub_ring) (void)hipHostFree(s->pub_ring);
+  if (s->gate_pin) (void)hipHostFree(s->gate_pin);
+  if (s->gate_dev) (void)hipFree(s->gate_dev);
   if (s->pub_count) (void)hipFree(s->pub_count);
   if (s->part) (void)hipFree(s->part);
   if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -2166,6 +2283,14 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   // bit for bit when coef is finite and no gl value is -0.0 or NaN, which the solver checked at
   // upload (pft_slab_set_gl_keep); XN's gl then already holds it, and stage 5 skips that store
   a.gl_keep = stage == 5 && kind == KFUSED && out && s->gl_keep && std::isfinite(coef) ? 1 : 0;
+  if (kind == KFUSED && s->gate_use_seq) {
+    // gated (pft_slab_gate_use): the scalars above are the launch's own (gate_scalars), from the
+    // decision the host has not taken yet; the kernel ANDs isfinite(coef) into gl_keep
+    const int j = (int)(s->gate_use_seq % PFT_GATE_SLOTS);
+    a.gate = s->gate_dev + 4 * j;
+    a.gseq = s->gate_use_seq;
+    a.gl_keep = stage == 5 && out && s->gl_keep ? 1 : 0;
+  }
   a.em0 = s->d.eps_mult[0];
   a.em1 = s->d.eps_mult[1];
   a.em2 = s->d.eps_mult[2];
@@ -2182,14 +2307,34 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
     s->pub_slot = j;
   }
   dim3 g((unsigned)(a.ntile * a.nchunk));
+  bool extra = false;
   if (stage == 1 && kind == KFUSED && s->defer_n > 0) {
     // the previous error-norm launch's partials: reduced and published by one extra workgroup
     a.part = s->part;
     a.npart = s->defer_n;
     a.pub = s->pub_ring_dev + 2 * s->defer_slot;
     s->defer_n = 0;
-    g.x += 1;
+    extra = true;
   }
+  if (stage == 1 && kind == KFUSED && s->gate_arm_seq && in) {
+    // the speculative stage 1 armed by pft_slab_gate_arm: its extra workgroup also decides the
+    // step that just ended, for the next step's pre-enqueued launches and for the host
+    const int j = (int)(s->gate_arm_seq % PFT_GATE_SLOTS);
+    a.gpin = s->gate_pin_dev + 4 * j;
+    a.gdev = s->gate_dev + 4 * j;
+    a.gdec_seq = s->gate_arm_seq;
+    a.dt = s->gate_arm_t;
+    a.dh = s->gate_arm_h;
+    a.d_final = s->gate_final;
+    a.d_delta = s->gate_delta;
+    a.d_hmin = s->gate_hmin;
+    a.d_local = s->gate_local;
+    a.d_nan = s->gate_nan;
+    __atomic_store_n(&s->gate_pin[4 * j], 0ULL, __ATOMIC_RELEASE);   // no decision yet
+    s->gate_arm_seq = 0;
+    extra = true;
+  }
+  if (extra) g.x += 1;
   const hipStream_t st = s->stream;
   if (gls)
     launch_stage<true>(stage, mode, kind, wx, g, st, a, s->c);
@@ -2429,6 +2574,82 @@ int pft_slab_timing_flush(pft_slab* s, double* ms, long* n)
 }
 
 int pft_slab_can_speculate(const pft_slab* s) { return slab_kind(s) == KFUSED; }
+
+// ---- gated steps (f4) ------------------------------------------------------------------------
+int pft_slab_gate_config(pft_slab* s, double final_time, double delta, double h_min, int delta_local, int handle_nan)
+{
+  s->gate_final = final_time;
+  s->gate_delta = delta;
+  s->gate_hmin = h_min;
+  s->gate_local = delta_local ? 1 : 0;
+  s->gate_nan = handle_nan ? 1 : 0;
+  return 0;
+}
+
+unsigned long long pft_slab_gate_arm(pft_slab* s, double t, double h)
+{
+  s->gate_arm_seq = ++s->gate_seq;
+  s->gate_arm_t = t;
+  s->gate_arm_h = h;
+  return s->gate_arm_seq;
+}
+
+int pft_slab_gate_decision(pft_slab* s, unsigned long long seq, int* go, double* t, double* h)
+{
+  // the device's decision (gate_decide), published right after the error norm the host has read
+  volatile unsigned long long* w = s->gate_pin + 4 * (seq % PFT_GATE_SLOTS);
+  long spins = 0;
+  unsigned long long v;
+  while (((v = __atomic_load_n(&w[0], __ATOMIC_ACQUIRE)) & ~PFT_GATE_SKIP) != seq) {
+    if (++spins < 200000) {
+      __builtin_ia32_pause();
+    } else if ((spins & 1023) == 0) {
+      const hipError_t q = hipStreamQuery(s->stream);
+      if (q != hipSuccess && q != hipErrorNotReady) return fail(q, "hipStreamQuery (gate decision poll)");
+      if (q == hipSuccess && ((__atomic_load_n(&w[0], __ATOMIC_ACQUIRE) & ~PFT_GATE_SKIP) != seq))
+        return fail(hipErrorUnknown, "gate decision never published");
+      sched_yield();
+    }
+  }
+  *go = v == seq;
+  const unsigned long long tb = w[1], hb = w[2];
+  memcpy(t, &tb, 8);
+  memcpy(h, &hb, 8);
+  return 0;
+}
+
+int pft_slab_gate_use(pft_slab* s, unsigned long long seq)
+{
+  s->gate_use_seq = seq;
+  return 0;
+}
+
+int pft_slab_book_save(pft_slab* s, int which)
+{
+  if (which < 0 || which > 1) return -2;
+  pft_slab::Book& b = s->book[which];
+  b.pub_next = s->pub_next;
+  b.pub_armed = s->pub_armed;
+  b.pub_slot = s->pub_slot;
+  b.eps_marked = s->eps_marked;
+  b.defer_n = s->defer_n;
+  b.defer_slot = s->defer_slot;
+  return 0;
+}
+
+int pft_slab_book_load(pft_slab* s, int which)
+{
+  if (which < 0 || which > 1) return -2;
+  const pft_slab::Book& b = s->book[which];
+  // pub_next only moves forward: a discarded gated launch may still publish into its slot
+  s->pub_next = std::max(s->pub_next, b.pub_next);
+  s->pub_armed = b.pub_armed;
+  s->pub_slot = b.pub_slot;
+  s->eps_marked = b.eps_marked;
+  s->defer_n = b.defer_n;
+  s->defer_slot = b.defer_slot;
+  return 0;
+}
 
 int pft_slab_stage_spec(pft_slab* s, double t_stage, int k_begin, int k_end)
 {

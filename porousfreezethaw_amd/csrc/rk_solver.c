@@ -24,6 +24,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 typedef struct {
 	int max_n;                    /* hybrid2.c:61; 0 = not initialised */
@@ -43,6 +44,7 @@ typedef struct {
 	int opt_gls, opt_kz, opt_dev, opt_timing, opt_tile, opt_norecompute;
 	int opt_lazy;               /* PFT_OPT_LAZY_ALLOC: device buffers at the first solve, not at init */
 	int opt_pair;               /* PFT_OPT_PAIR: stages 2+3 and 4+5 as pair kernels where the slab can */
+	int opt_gate;               /* PFT_OPT_GATE: gated steps on small single slabs (f4) */
 	int deep;                   /* this call runs the pair kernels on z-neighbouring slabs: every stage
 	                               launch covers the whole slab and is followed by the two-plane halo
 	                               exchange of its output (pft_comm_halo_deep) */
@@ -56,7 +58,7 @@ typedef struct {
 	pft_solver_stats stats;
 } solver_state;
 
-static __thread solver_state R = { .slab_dev = -1, .opt_kz = 0, .opt_dev = -1, .opt_tile = 1, .opt_pair = 1 };
+static __thread solver_state R = { .slab_dev = -1, .opt_kz = 0, .opt_dev = -1, .opt_tile = 1, .opt_pair = 1, .opt_gate = 1 };
 
 static pft_comm * comm(void)
 {
@@ -163,6 +165,7 @@ int pft_solver_set_option(int opt, long value)
 		case PFT_OPT_LAZY_ALLOC: R.opt_lazy = value ? 1 : 0; return 0;
 		case PFT_OPT_FAIL_RHS: if(value < 0) return -2; R.fail_rhs_after = value; R.rhs_calls = 0; return 0;
 		case PFT_OPT_PAIR: if(value < 0 || value > 2) return -2; R.opt_pair = (int)value; return 0;
+		case PFT_OPT_GATE: if(value < 0 || value > 1) return -2; R.opt_gate = (int)value; return 0;
 		case PFT_OPT_RECOMPUTE:
 			R.opt_norecompute = value ? 0 : 1; if(R.slab) pft_slab_set_recompute(R.slab, !R.opt_norecompute); return 0;
 		case PFT_OPT_TILE:
@@ -355,6 +358,14 @@ typedef struct {
 static int run_staged(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast * B, int command,
                       long max_steps_total, int flags);
 
+/* PFT_GATE_TRACE=1: host-side timeline of the gated pipeline (stderr at the end of a call) */
+static double gt_now(void)
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
 static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast * B, int command,
                      long max_steps_total, int flags, const double * em)
 {
@@ -366,6 +377,10 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	long attempted = 0, launches = 0;
 	int spec, k1_valid = 0;               /* K1 holds f(t, x) for the current t and x */
 	int pair;                             /* stages 2+3 and 4+5 as pair kernels */
+	int gate, pre = 0, acc, enq;          /* gated steps; this attempt was pre-enqueued; accepted;
+	                                         the next attempt is pre-enqueued */
+	unsigned long long gcur = 0, gnext;   /* decisions on this attempt (by its speculative stage 1)
+	                                         and on the pre-enqueued one */
 
 	if((rc = ensure_slab())) return rc;
 	pft_slab_set_eps_mult(R.slab, em);
@@ -386,6 +401,8 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	}
 	R.deep = pair && pft_comm_splits(c);
 	R.stats.pairs = pair;
+	R.stats.gated_steps = 0;
+	R.stats.gate_misses = 0;
 	if(!(flags & PFT_SOLVE_REUSE_DEVICE) || !R.device_valid) {
 		if((rc = pft_slab_upload_host(R.slab, PFT_BUF_X, system->x))) return rc;
 		if((rc = pft_slab_upload_host(R.slab, PFT_BUF_XN, system->x))) return rc;
@@ -418,35 +435,95 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 		pft_slab_set_inkernel_publish(R.slab, on);
 	}
 
+	/* f4, gated steps (PFT_OPT_GATE, pft_slab_gate_*): on one slab with one launch per stage, the
+	   next attempted step's launches are enqueued before this step's error norm is read, as if the
+	   step were accepted.  This step's speculative stage 1 reduces the error norm and decides the
+	   step on the device (hybrid2.c:578-611, the expressions below); the gated launches run on
+	   that decision, so the GPU waits neither for the host's round trip nor for its launch latency.
+	   The host still takes the decision below (glibc pow) and keeps the gated step only if the
+	   device's (ocml pow) is the same bit for bit; otherwise that step is discarded -- it wrote only
+	   buffers nothing reads afterwards (XN, A0, K3, K4, A1) -- and launched again.  Not with a
+	   Service_Callback (it may read x between steps) or per-stage timing. */
+	gate = R.opt_gate && spec && !pair && nprocs == 1 && !pft_comm_splits(c) &&
+	       system->Service_Callback == NULL && !R.opt_timing;
+	if(gate) pft_slab_gate_config(R.slab, final_time, delta, h_min, B->delta_mode == DELTA_LOCAL, B->handle_nan);
+	const int gtrace = getenv("PFT_GATE_TRACE") != NULL;
+	double gt_t0 = 0.0, gt_enq = 0.0, gt_wait = 0.0, gt_dec = 0.0, gt_a, gt_b;
+	long gt_n = 0;
+	if(gtrace) gt_t0 = gt_now();
+
 	while(1) {
 		h2 = h/2.0; h3 = h/3.0; h6 = h/6.0; h8 = h/8.0;                          /* :355 */
 		R.tstep = R.opt_timing > 0 && attempted % R.opt_timing == 0;
-		/* the error norm accumulator is reset by its publication on the speculative path */
-		if((!spec || attempted == 0) && (rc = pft_slab_eps_reset(R.slab))) return rc;
-		/* K1 = f(t,x); aux = x + K1 h/3 ... K5 = f(t+h, aux); error norm; x(t+h) candidate */
-		if(pair) {
-			/* the same arithmetic: stage A of each pair is evaluated inside stage B's stencil */
-			if(!k1_valid && (rc = do_stage(1, t, h3, h, &launches))) return rc;      /* :373-389 */
-			if((rc = do_pair(2, t+h3, t+h3, h, h3, &launches))) return rc;          /* :392-429 */
-			if((rc = do_pair(4, t+h2, t+h, h, h3, &launches))) return rc;           /* :432-524,657-668 */
-		} else {
-			if(!(spec && k1_valid) && (rc = do_stage(1, t, h3, h, &launches))) return rc;  /* :373-389 */
-			if((rc = do_stage(2, t+h3, h6, h, &launches))) return rc;    /* :392-409 */
-			if((rc = do_stage(3, t+h3, h8, h, &launches))) return rc;    /* :412-429 */
-			if((rc = do_stage(4, t+h2, h,  h, &launches))) return rc;    /* :432-450 */
-			if((rc = do_stage(5, t+h,  h3, h, &launches))) return rc;    /* :453,507-524,657-668 */
+		acc = 0;
+		if(!pre) {
+			/* the error norm accumulator is reset by its publication on the speculative path */
+			if((!spec || attempted == 0) && (rc = pft_slab_eps_reset(R.slab))) return rc;
+			/* K1 = f(t,x); aux = x + K1 h/3 ... K5 = f(t+h, aux); error norm; x(t+h) candidate */
+			if(pair) {
+				/* the same arithmetic: stage A of each pair is evaluated inside stage B's stencil */
+				if(!k1_valid && (rc = do_stage(1, t, h3, h, &launches))) return rc;      /* :373-389 */
+				if((rc = do_pair(2, t+h3, t+h3, h, h3, &launches))) return rc;          /* :392-429 */
+				if((rc = do_pair(4, t+h2, t+h, h, h3, &launches))) return rc;           /* :432-524,657-668 */
+			} else {
+				if(!(spec && k1_valid) && (rc = do_stage(1, t, h3, h, &launches))) return rc;  /* :373-389 */
+				if((rc = do_stage(2, t+h3, h6, h, &launches))) return rc;    /* :392-409 */
+				if((rc = do_stage(3, t+h3, h8, h, &launches))) return rc;    /* :412-429 */
+				if((rc = do_stage(4, t+h2, h,  h, &launches))) return rc;    /* :432-450 */
+				if((rc = do_stage(5, t+h,  h3, h, &launches))) return rc;    /* :453,507-524,657-668 */
+			}
+			k1_valid = 1;
+			if(spec) {
+				/* eps max over ranks (:572) and its publication beside the speculative stage 1 */
+				if((rc = pft_comm_eps_publish(c))) return rc;
+				if(gate) gcur = pft_slab_gate_arm(R.slab, t, h);
+				if((rc = do_stage(6, t+h, 0.0, h, &launches))) return rc;
+			} else {
+				/* the boundary launch of stage 5 (comm stream) adds to the error norm too */
+				if(pft_comm_splits(c) && (rc = pft_slab_order(R.slab, 1))) return rc;
+				if((rc = pft_comm_allreduce_eps(c))) return rc;                      /* :572 */
+			}
 		}
-		k1_valid = 1;
-		if(spec) {
-			/* eps max over ranks (:572) and its publication beside the speculative stage 1 */
-			if((rc = pft_comm_eps_publish(c))) return rc;
-			if((rc = do_stage(6, t+h, 0.0, h, &launches))) return rc;
-		} else {
-			/* the boundary launch of stage 5 (comm stream) adds to the error norm too */
-			if(pft_comm_splits(c) && (rc = pft_slab_order(R.slab, 1))) return rc;
-			if((rc = pft_comm_allreduce_eps(c))) return rc;                      /* :572 */
+		pre = 0;
+		gnext = 0;
+		gt_a = gtrace ? gt_now() : 0.0;
+		/* pre-enqueue the next attempt unless this one ends the solve if accepted (FINISHED) or the
+		   step cap stops before it */
+		enq = gate && gcur && !(command & RKA_CMD_FINISHED) &&
+		      !(max_steps_total > 0 && attempted + 1 >= max_steps_total);
+		if(enq) {
+			/* the next attempted step, enqueued now as if this one were accepted (the buffers
+			   swapped as the accept below swaps them, for the enqueue only): stages 2-5 and its
+			   speculative stage 1, gated on the device's decision gcur.  The scalars passed here
+			   are not used: the launches derive theirs from the decided (t, h). */
+			pft_slab_book_save(R.slab, 0);
+			pft_slab_accept(R.slab);
+			pft_slab_swap_buffers(R.slab, PFT_BUF_K1, PFT_BUF_A1);
+			pft_slab_gate_use(R.slab, gcur);
+			rc = 0;
+			if(!rc) rc = do_stage(2, 0.0, 0.0, 0.0, &launches);
+			if(!rc) rc = do_stage(3, 0.0, 0.0, 0.0, &launches);
+			if(!rc) rc = do_stage(4, 0.0, 0.0, 0.0, &launches);
+			if(!rc) rc = do_stage(5, 0.0, 0.0, 0.0, &launches);
+			if(!rc) rc = pft_comm_eps_publish(c);
+			if(!rc) gnext = pft_slab_gate_arm(R.slab, 0.0, 0.0);   /* (t, h) from its own gate */
+			if(!rc) rc = do_stage(6, 0.0, 0.0, 0.0, &launches);
+			pft_slab_gate_use(R.slab, 0);
+			pft_slab_accept(R.slab);
+			pft_slab_swap_buffers(R.slab, PFT_BUF_K1, PFT_BUF_A1);
+			pft_slab_book_save(R.slab, 1);
+			pft_slab_book_load(R.slab, 0);
+			if(rc) return rc;
 		}
+		gt_b = gtrace ? gt_now() : 0.0;
 		if((rc = pft_slab_eps_fetch(R.slab, &eps, &nonfinite))) return rc;
+		if(gtrace) {
+			const double n = gt_now();
+			gt_enq += gt_b - gt_a;
+			gt_wait += n - gt_b;
+			gt_a = n;
+			gt_n++;
+		}
 		if((rc = pft_comm_eps_host(c, &eps, &nonfinite))) return rc;                 /* :572 (ipc) */
 		if(R.opt_timing) pft_slab_timing_collect(R.slab, R.stats.stage_ms, R.stats.stage_n);
 		system->steps_total++;                                                   /* :460 */
@@ -472,6 +549,7 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 		} else {
 			if(command & RKA_CMD_UPDATE) {                                       /* :651-668 */
 				t += h;
+				acc = 1;
 				pft_slab_accept(R.slab);
 				if(spec) pft_slab_swap_buffers(R.slab, PFT_BUF_K1, PFT_BUF_A1);  /* K1 = f(t, x) */
 				else k1_valid = 0;
@@ -515,7 +593,31 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 			break;
 		}
 		if(to_host) break;
+		if(enq) {
+			/* keep the pre-enqueued attempt iff the device took this decision, bit for bit:
+			   accepted, and the same next t and h (its launches ran on them); otherwise it
+			   exited at once (device: rejected) or ran on a different h (pow) and is discarded */
+			int go = 0;
+			double td = 0.0, hd = 0.0;
+			if((rc = pft_slab_gate_decision(R.slab, gcur, &go, &td, &hd))) return rc;
+			if(gtrace) gt_dec += gt_now() - gt_a;
+			if(acc && go && memcmp(&td, &t, sizeof t) == 0 && memcmp(&hd, &h, sizeof h) == 0) {
+				pft_slab_book_load(R.slab, 1);
+				pre = 1;
+				R.stats.gated_steps++;
+				gcur = gnext;
+			} else {
+				if(acc && go) R.stats.gate_misses++;
+				gcur = 0;
+			}
+		} else {
+			gcur = 0;
+		}
 	}
+	if(gtrace && gt_n)
+		fprintf(stderr, "libpft gate trace: %ld attempts, %.2f us each: enqueue %.2f, eps wait %.2f, "
+		        "decide+compare %.2f (gated %ld, pow misses %ld)\n", gt_n, (gt_now() - gt_t0) / gt_n,
+		        gt_enq / gt_n, gt_wait / gt_n, gt_dec / gt_n, R.stats.gated_steps, R.stats.gate_misses);
 	(void)rank;
 	/* join the comm stream (the last boundary launch and exchange) before the state leaves */
 	if(pft_comm_splits(c) && (rc = pft_slab_order(R.slab, 1))) return rc;
