@@ -84,8 +84,8 @@ def parse():
     ap.add_argument("--no-recompute", action="store_true",
                     help="materialise the reference's aux arrays between stages (72 vs 54 doubles/cell-step)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
-    ap.add_argument("--gate", type=int, default=1, choices=(0, 1),
-                    help="gated steps on small single slabs (PFT_OPT_GATE, f4; 0: off for A/B)")
+    ap.add_argument("--gate", type=int, default=0, choices=(0, 1),
+                    help="gated steps on small single slabs (PFT_OPT_GATE, f4; default off: measured neutral)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="CPU sample: attempted steps (in batches of 2) until this much time has passed")
     ap.add_argument("--no-timing", action="store_true", help="no HIP-event stage timing")

@@ -67,11 +67,13 @@ enum {
 	PFT_OPT_FAIL_RHS = 11,  /* test hook: N > 0 makes the N-th device evaluation of libpft's own
 	                           right-hand side on a host array (f_generic_model01/2 called by the
 	                           host-staged path) fail as a device fault would; 0 (default) off */
-	PFT_OPT_GATE = 12       /* gated steps (f4): 1 (default) = on one slab with one launch per
-	                           stage and no Service_Callback, the next attempted step's launches are
-	                           enqueued before this step's error norm is read and run on the
-	                           device's step decision, which the host checks bit for bit
-	                           (pft_slab_gate_*); 0 = off.  Bit-identical either way. */
+	PFT_OPT_GATE = 12       /* gated steps (f4): 1 = on one slab with one launch per stage and no
+	                           Service_Callback, the next attempted step's launches are enqueued
+	                           before this step's error norm is read and run on the device's step
+	                           decision, which the host checks bit for bit (pft_slab_gate_*);
+	                           0 (default) = off: measured neutral at 100^3 (38.2 vs 37.4-38.5 us
+	                           per attempted step) and -2% at 200^3, where the step is bound by its
+	                           kernels, not by the host.  Bit-identical. */
 };
 int pft_solver_set_option(int opt, long value);
 

@@ -278,12 +278,56 @@ __device__ __forceinline__ void gate_scalars(StageArgs& a, const pft_consts& c, 
   if (STAGE == 5) a.gl_keep = a.gl_keep && isfinite(a.coef);
 }
 
+// x^0.2 rounded to nearest, for the step-size control.  glibc's pow (the host's) rounds correctly
+// but for rare hard cases; ocml's is within ~1 ulp (10% of the decisions differed in the last
+// bit).  So the candidate c = pow(x, 0.2) is checked against the midpoints to its neighbours in
+// double-double arithmetic: v = x^0.2 > m  <=>  x > m^(1/0.2), and 1/0.2 = 5 / (1 + 5 e) with
+// 0.2 = 1/5 + e, e = 2^-54 / 5, so m^(1/0.2) = m^5 (1 - 25 e ln m) to far below the ~2^-53 the
+// comparison needs.  Outside a safe range the candidate stays (the host's check catches it).
+struct pft_dd {
+  double hi, lo;
+};
+__device__ __forceinline__ pft_dd dd_norm(double a, double b)
+{
+  const double s = a + b;
+  return {s, b - (s - a)};
+}
+__device__ __forceinline__ pft_dd dd_mul(pft_dd a, pft_dd b)
+{
+  const double p = a.hi * b.hi;
+  double e = fma(a.hi, b.hi, -p);
+  e += a.hi * b.lo + a.lo * b.hi;
+  return dd_norm(p, e);
+}
+// sign of x - m^(1/0.2) for the midpoint m = c + d (d = half the gap to a neighbour of c)
+__device__ __forceinline__ int pow02_side(double x, double c, double d, double k)
+{
+  const pft_dd m = {c, d};
+  const pft_dd m2 = dd_mul(m, m), m4 = dd_mul(m2, m2), m5 = dd_mul(m4, m);
+  // T = m5 (1 - k): m5.hi - m5.hi k + m5.lo
+  const double corr = -(m5.hi * k) + m5.lo;
+  const double s = x - m5.hi;                 // exact when x and m5.hi are close (Sterbenz)
+  const double r = s - corr;
+  return r > 0.0 ? 1 : (r < 0.0 ? -1 : 0);
+}
+__device__ __forceinline__ double pow02_rn(double x)
+{
+  const double c = pow(x, 0.2);
+  if (!(x > 0x1p-900 && x < 0x1p900) || !(c > 0.0 && c < 0x1p200)) return c;
+  const double k = 25.0 * (0x1p-54 / 5.0) * log(c);
+  const double up = nextafter(c, INFINITY), dn = nextafter(c, 0.0);
+  if (pow02_side(x, c, 0.5 * (up - c), k) > 0) return up;
+  if (pow02_side(x, c, 0.5 * (dn - c), k) < 0) return dn;
+  return c;
+}
+
 // One thread: the step-size control of hybrid2.c:578-611 (rk_solver.c run_fused_impl restates it
 // on the host) for the step (t, h) whose error norm bits epsb / non-finite flag nf were just
 // reduced: the next step's (t, h) when it is accepted, a skip when it is rejected or hit a NaN.
-// The only operation not correctly rounded is pow (ocml here, glibc on the host): the host takes
-// its own decision and runs the gated step only if both agree bit for bit (otherwise it discards
-// it and launches the step again with its own h).
+// pow is the only operation not correctly rounded by IEEE: pow02_rn here, glibc on the host,
+// which agree but for glibc's rare misrounded cases; the host takes its own decision and keeps
+// the gated step only if both agree bit for bit (otherwise it discards it and launches the step
+// again with its own h).
 __device__ __forceinline__ void gate_decide(const StageArgs& a, double t, double h, unsigned long long epsb, int nf,
                                             bool have_eps)
 {
@@ -292,7 +336,7 @@ __device__ __forceinline__ void gate_decide(const StageArgs& a, double t, double
   if (have_eps && !(a.d_nan && nf)) {                                      // :493-503
     const double h3 = h / 3.0;
     if (a.d_local) eps *= fabs(h3);                                        // :578
-    const double new_h = ((eps > 0.0) ? pow((a.d_delta / eps), 0.2) * 0.8 : 2.0) * h;   // :580
+    const double new_h = ((eps > 0.0) ? pow02_rn((a.d_delta / eps)) * 0.8 : 2.0) * h;   // :580
     if (eps < a.d_delta || fabs(h) < a.d_hmin) {                           // :599-611
       const double tn = t + h;                                             // :652
       const double hn = (fabs(a.d_final - tn) <= fabs(new_h)) ? a.d_final - tn : new_h;   // :743-761

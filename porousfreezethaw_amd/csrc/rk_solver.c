@@ -58,7 +58,7 @@ typedef struct {
 	pft_solver_stats stats;
 } solver_state;
 
-static __thread solver_state R = { .slab_dev = -1, .opt_kz = 0, .opt_dev = -1, .opt_tile = 1, .opt_pair = 1, .opt_gate = 1 };
+static __thread solver_state R = { .slab_dev = -1, .opt_kz = 0, .opt_dev = -1, .opt_tile = 1, .opt_pair = 1, .opt_gate = 0 };
 
 static pft_comm * comm(void)
 {

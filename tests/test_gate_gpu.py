@@ -1,13 +1,16 @@
-"""f4, gated steps (PFT_OPT_GATE, rk_solver.c run_fused_impl, pft_slab_gate_*): on a small single
-slab the launches of the next attempted step are enqueued before the host has read this step's
-error norm and run on the host's decision.  Every test compares against the reference itself
-(tests/golden/g100.json, BASELINE configs[0], produced by the reference compiled in place) or
-against the same solve with gating off: t, h, step counts and the fields bit for bit.
+"""f4, gated steps (PFT_OPT_GATE, rk_solver.c run_fused, pft_slab_gate_*; off by default): on a
+small single slab the launches of the next attempted step are enqueued before this step's error
+norm is known and run on the device's own step decision (the speculative stage 1 reduces the error
+norm and decides as hybrid2.c:578-611, with a correctly rounded x^0.2); the host takes its own
+decision with glibc's pow and keeps the gated step only if both agree bit for bit.  Every test
+compares against the reference itself (tests/golden/g100.json, BASELINE configs[0], produced by
+the reference compiled in place) or against the same solve with gating off: t, h, step counts and
+the fields bit for bit.
 
-Paths covered: accepted steps (go), rejected steps (skip; the next attempt ungated), the last step
-to final_time (NEXTFINISH / FINISHED), step caps of pft_solve_ex at every phase of the pipeline
-(the armed decision released on exit), calls that continue a resident state, and the bounded wait
-on the device (a decision never written ends as a skip, tested through the solver's own exits).
+Paths covered: accepted steps (kept), rejected steps (the gated launches exit at once; the next
+attempt ungated), the last step to final_time (NEXTFINISH / FINISHED: no gated step after it),
+step caps of pft_solve_ex at every phase of the pipeline, calls that continue a resident state,
+and RK_MPI_SA_solve's host boundary after a discarded gated step.
 """
 import hashlib
 
@@ -32,9 +35,10 @@ def g100():
 
 
 @pytest.fixture(autouse=True)
-def _gate_default():
+def _gate_on():
+    P.lib().pft_solver_set_option(P.PFT_OPT_GATE, 1)      # off by default
     yield
-    P.lib().pft_solver_set_option(P.PFT_OPT_GATE, 1)
+    P.lib().pft_solver_set_option(P.PFT_OPT_GATE, 0)
 
 
 def _sim(meta):
@@ -66,6 +70,9 @@ def test_gated_g100_reference_trajectory(g100):
         st = sim.stats()
         assert st.path == 1 and not st.pairs
         gated += st.gated_steps
+        # the device's x^0.2 is correctly rounded: it differs from glibc's only where glibc
+        # misrounds (~0.06% of random arguments), and each difference costs one discarded step
+        assert st.gate_misses <= max(2, st.gated_steps // 50), (st.gate_misses, st.gated_steps)
     accepted = meta["traj_m0"][-1][2]
     assert gated >= accepted // 2, (gated, accepted)
     sim.close()
