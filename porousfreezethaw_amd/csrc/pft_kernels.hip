@@ -1372,8 +1372,13 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
       if (SA == 4) __builtin_amdgcn_s_setprio(0);
       else if ((threadIdx.x >> 8) == 0) __builtin_amdgcn_s_setprio(0);
       else __builtin_amdgcn_s_setprio(2);
-      // operands of plane kB for stage B's outputs (4+5), after stage A: fewer registers live
-      // during stage A, and the latency hides behind stage B's stencil
+      // operands of plane kB for stage B's outputs (4+5), loaded a second time, after stage A:
+      // fewer registers live during stage A (keeping them would need ~60 VGPRs more than the 255
+      // in use), and the latency hides behind stage B's stencil.  NOT an L2 hit: their first load
+      // was the look-ahead three planes earlier, and three planes of the ring's operands of the
+      // ~32 workgroups of an XCD (~5 MB) exceed its 4 MB L2 -- the Infinity Cache serves them
+      // (PMC: 1.78x the algorithmic bytes beyond L2; skipping the re-load in
+      // an ablation gained ~1%)
       // (GLX: gl's x(t+h) is not stored, XN holds it: gl's x is not needed)
       // (unconditional, as the look-ahead: every lane's acting pair is in the domain)
       if (SA == 4 && kB >= kb && isB) pair_load<SA, !GLX>(A2, pbo(kB), ro);
