@@ -14,10 +14,14 @@ O=gpurun_out/ev
 mkdir -p $O/prof
 fatal() { local rc=$1; echo "[$2] exit $rc" | tee -a $O/status.log
   if [ "$rc" -ge 124 ] || [ "$rc" -eq 134 ] || [ "$rc" -eq 139 ]; then echo "fatal in $2, stopping"; exit "$rc"; fi; }
-if [ -z "$SKIP_TESTS" ]; then
+# PART=1: tests, smoke, traces, PMC passes and the default bench line; PART=2: the other
+# workloads; unset: both (a gpurun call is limited to 20 minutes)
+PART=${PART:-all}
+if [ "$PART" != 2 ] && [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $O/pytest_gpu.log 2>&1; fatal $? pytest
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1; fatal $? smoke
 fi
+if [ "$PART" != 2 ]; then
 ARGS="--steps 20 --warmup 3 --no-cpu --probe 3"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof/trace -o run --output-format csv -- python3 bench.py $ARGS > $O/prof/trace_bench.json 2> $O/prof/trace.err; fatal $? trace
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $O/prof/fetch -o run --output-format csv -- python3 bench.py $ARGS > $O/prof/fetch_bench.json 2> $O/prof/fetch.err; fatal $? fetch
@@ -28,6 +32,10 @@ PB=$(python3 -c "import json;print(json.load(open('$O/prof/trace_bench.json'))['
 python3 scripts/pmc_summary.py $O/prof/trace $O/prof/fetch $O/prof/write 200x200x400 $PB $O/pmc_summary.json $O/prof/valu $O/prof/fp64 > $O/pmc_summary.txt 2>&1; fatal $? pmc_summary
 cp $O/pmc_summary.json profiles/pmc_summary.json
 timeout -k 10 900 python bench.py > $O/bench_default.json 2> $O/bench_default.err; fatal $? bench_default
+# the GPU clock per launch in the driver's configuration, with the bench's clock pre-warm
+timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE -d $O/prof/clk -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu > $O/prof/clk_bench.json 2> $O/prof/clk.err; fatal $? clock
+fi
+[ "$PART" = 1 ] && { echo done >> $O/status.log; exit 0; }
 PFT_PAIR=0 timeout -k 10 300 python bench.py --steps 100 --no-cpu > $O/bench_nopair.json 2>> $O/bench_var.err; fatal $? bench_nopair
 timeout -k 10 300 python bench.py --steps 100 --no-cpu --mode 1 > $O/bench_mode1.json 2>> $O/bench_var.err; fatal $? bench_mode1
 timeout -k 10 300 python bench.py --steps 100 --no-cpu --mode 2 > $O/bench_mode2.json 2>> $O/bench_var.err; fatal $? bench_mode2
