@@ -444,7 +444,12 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	   device's (ocml pow) is the same bit for bit; otherwise that step is discarded -- it wrote only
 	   buffers nothing reads afterwards (XN, A0, K3, K4, A1) -- and launched again.  Not with a
 	   Service_Callback (it may read x between steps) or per-stage timing. */
-	gate = R.opt_gate && spec && !pair && nprocs == 1 && !pft_comm_splits(c) &&
+	{
+		/* env PFT_GATE=0/1 overrides PFT_OPT_GATE (whole-suite runs with gating forced on) */
+		const char * eg = getenv("PFT_GATE");
+		gate = eg ? atoi(eg) != 0 : R.opt_gate;
+	}
+	gate = gate && spec && !pair && nprocs == 1 && !pft_comm_splits(c) &&
 	       system->Service_Callback == NULL && !R.opt_timing;
 	if(gate) pft_slab_gate_config(R.slab, final_time, delta, h_min, B->delta_mode == DELTA_LOCAL, B->handle_nan);
 	const int gtrace = getenv("PFT_GATE_TRACE") != NULL;
