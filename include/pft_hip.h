@@ -178,6 +178,9 @@ int pft_slab_gate_config(pft_slab * s, double final_time, double delta, double h
 unsigned long long pft_slab_gate_arm(pft_slab * s, double t, double h);
 int pft_slab_gate_use(pft_slab * s, unsigned long long seq);
 int pft_slab_gate_decision(pft_slab * s, unsigned long long seq, int * go, double * t, double * h);
+/* x^0.2 rounded to nearest from a candidate c within 1 ulp (the device's gate_decide uses it with
+   ocml's pow as c): host build of the same code, for the CPU tests */
+double pft_pow02_fix(double x, double c);
 int pft_slab_book_save(pft_slab * s, int which);
 int pft_slab_book_load(pft_slab * s, int which);
 /* Pair kernels (one slab, recompute path): stages 2+3 or 4+5 of the step (first = 2 or 4) in ONE

@@ -287,12 +287,12 @@ __device__ __forceinline__ void gate_scalars(StageArgs& a, const pft_consts& c, 
 struct pft_dd {
   double hi, lo;
 };
-__device__ __forceinline__ pft_dd dd_norm(double a, double b)
+__host__ __device__ __forceinline__ pft_dd dd_norm(double a, double b)
 {
   const double s = a + b;
   return {s, b - (s - a)};
 }
-__device__ __forceinline__ pft_dd dd_mul(pft_dd a, pft_dd b)
+__host__ __device__ __forceinline__ pft_dd dd_mul(pft_dd a, pft_dd b)
 {
   const double p = a.hi * b.hi;
   double e = fma(a.hi, b.hi, -p);
@@ -300,7 +300,7 @@ __device__ __forceinline__ pft_dd dd_mul(pft_dd a, pft_dd b)
   return dd_norm(p, e);
 }
 // sign of x - m^(1/0.2) for the midpoint m = c + d (d = half the gap to a neighbour of c)
-__device__ __forceinline__ int pow02_side(double x, double c, double d, double k)
+__host__ __device__ __forceinline__ int pow02_side(double x, double c, double d, double k)
 {
   const pft_dd m = {c, d};
   const pft_dd m2 = dd_mul(m, m), m4 = dd_mul(m2, m2), m5 = dd_mul(m4, m);
@@ -310,9 +310,9 @@ __device__ __forceinline__ int pow02_side(double x, double c, double d, double k
   const double r = s - corr;
   return r > 0.0 ? 1 : (r < 0.0 ? -1 : 0);
 }
-__device__ __forceinline__ double pow02_rn(double x)
+// c: a candidate within 1 ulp of x^0.2 (ocml's pow on the device)
+__host__ __device__ __forceinline__ double pow02_fix(double x, double c)
 {
-  const double c = pow(x, 0.2);
   if (!(x > 0x1p-900 && x < 0x1p900) || !(c > 0.0 && c < 0x1p200)) return c;
   const double k = 25.0 * (0x1p-54 / 5.0) * log(c);
   const double up = nextafter(c, INFINITY), dn = nextafter(c, 0.0);
@@ -320,6 +320,7 @@ __device__ __forceinline__ double pow02_rn(double x)
   if (pow02_side(x, c, 0.5 * (dn - c), k) < 0) return dn;
   return c;
 }
+__device__ __forceinline__ double pow02_rn(double x) { return pow02_fix(x, pow(x, 0.2)); }
 
 // One thread: the step-size control of hybrid2.c:578-611 (rk_solver.c run_fused_impl restates it
 // on the host) for the step (t, h) whose error norm bits epsb / non-finite flag nf were just
@@ -2625,6 +2626,10 @@ int pft_slab_timing_flush(pft_slab* s, double* ms, long* n)
 int pft_slab_can_speculate(const pft_slab* s) { return slab_kind(s) == KFUSED; }
 
 // ---- gated steps (f4) ------------------------------------------------------------------------
+// the device's x^0.2 correction (pow02_fix) compiled for the host: CPU tests check it against a
+// high-precision reference with candidates one ulp off either way (tests/test_pow02.py)
+double pft_pow02_fix(double x, double c) { return pow02_fix(x, c); }
+
 int pft_slab_gate_config(pft_slab* s, double final_time, double delta, double h_min, int delta_local, int handle_nan)
 {
   s->gate_final = final_time;
