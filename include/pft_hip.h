@@ -226,15 +226,20 @@ int pft_probe_copy(double * dst, const double * src, size_t n, void * stream);
 
 /* ipc transport (pft_comm.h).  Every rank swaps its buffers identically, so a buffer role names
    the same physical allocation on every slab; the neighbours' allocations are mapped once.
-   export: the slab's PFT_BUF_COUNT buffer allocations + its flag words as PFT_BUF_COUNT + 1
-   hipIpcMemHandle_t (64 bytes each, PFT_IPC_HANDLE_BYTES in all);
+   export: the slab's PFT_BUF_COUNT buffer allocations, its flag words and its receive buffer as
+   PFT_BUF_COUNT + 2 hipIpcMemHandle_t (64 bytes each, PFT_IPC_HANDLE_BYTES in all);
    set_peer(side 0 = below / 1 = above): open the neighbour's handles (handles = NULL: the slab
    itself, the one-GPU self-exchange diagnostic); n3 / fs are the neighbour's planes and stride;
    halo_put: boundary planes 1 and n3 of buffer `role`, fields [f0, f1), into the neighbours' ghost
    planes, then `seq` into their flag words (a copy and a one-thread signal kernel on the compute
    stream);
-   halo_wait: the compute stream waits until both neighbours' flags reach `seq`. */
-#define PFT_IPC_HANDLE_BYTES (64 * (PFT_BUF_COUNT + 1))
+   halo_wait: the compute stream waits until both neighbours' flags reach `seq`.
+   Staged receive (a neighbour on another GPU, or env PFT_IPC_STAGED=1): the sender writes into the
+   receiver's receive buffer -- uncached device memory, so no cache of the receiving GPU holds a
+   line of it -- instead of its ghost planes, and after the flag wait the receiver copies it into
+   its ghost planes on its own stream (halo_recv_kernel): the halo is then as coherent as any
+   kernel-to-kernel hand-off on one GPU, whatever the receiving L2s held of the ghost planes. */
+#define PFT_IPC_HANDLE_BYTES (64 * (PFT_BUF_COUNT + 2))
 int pft_slab_ipc_export(pft_slab * s, void * handles);
 int pft_slab_ipc_set_peer(pft_slab * s, int side, const void * handles, int n3, long fs, int device);
 int pft_slab_ipc_close(pft_slab * s);
@@ -253,8 +258,7 @@ int pft_slab_halo_wait(pft_slab * s, unsigned long long seq);
    slab (this one, up/download, the error-norm fetch) is bounded by PFT_IPC_TIMEOUT seconds
    (default 300): a peer that died or diverged never raises the flag the stream waits on, so on
    expiry the slab releases its own flags, drains the stream and returns PFT_ERR_IPC_TIMEOUT
-   (RK_MPI_SA_solve: PFT_SOLVE_DEVICE_ERROR).  set_peer refuses (-2) a neighbour on another GPU
-   unless PFT_IPC_CROSS_GPU=1: cross-GPU ipc halos are not verified on hardware. */
+   (RK_MPI_SA_solve: PFT_SOLVE_DEVICE_ERROR).  A neighbour on another GPU is staged (above). */
 #define PFT_ERR_IPC_TIMEOUT (-5002)
 int pft_slab_sync(pft_slab * s);
 

@@ -1623,6 +1623,34 @@ __global__ __launch_bounds__(256) void halo_put_kernel(PutArgs a)
   }
 }
 
+// Staged receive (pft_slab_halo_wait): the planes the neighbours put into this slab's receive
+// buffer rbuf (uncached; two slots by the exchange's parity, each [side][depth][field][plane], side
+// 0 from below, 1 from above; depth 0 the ghost plane, 1 the far ghost plane) copied into the ghost planes of buffer dst, fields
+// [f0, f0 + nf), for the sides in `sides` (bit 0 below, bit 1 above)
+struct RecvArgs {
+  const double* rbuf;
+  double* dst;                // the buffer (pft_slab_buffer layout: plane 0 = ghost below)
+  long fs;
+  int plane, n3, f0, nf, depth, sides;
+};
+
+__global__ __launch_bounds__(256) void halo_recv_kernel(RecvArgs a)
+{
+  const long n = (long)a.nf * a.plane;
+  const long tot = 4L * n;              // (side, depth) parts, skipped where not received
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
+    const int part = (int)(e / n);
+    const int side = part >> 1, depth = part & 1;
+    if (!((a.sides >> side) & 1) || depth >= a.depth) continue;
+    const long r = e - part * n;
+    const int f = (int)(r / a.plane);
+    const long c = r - (long)f * a.plane;
+    const int q = a.f0 + f;
+    const long pl = side == 0 ? (depth == 0 ? 0L : -1L) : (long)a.n3 + 1 + depth;
+    a.dst[q * a.fs + pl * a.plane + c] = a.rbuf[((long)(side * 2 + depth) * 3 + q) * a.plane + c];
+  }
+}
+
 // raises the neighbours' flags once the kernels before it on the stream (the put, or a stage
 // kernel that stored its boundary planes into the neighbours' ghost planes) have completed: their
 // stores are released at kernel end; with a neighbour on another GPU a system-scope fence first
@@ -1659,6 +1687,8 @@ struct SlabPeer {
   long fs;                             // its field stride
   int n3;                              // its interior planes
   int remote;                          // 1: on another GPU (xGMI)
+  int staged;                          // 1: our planes go to its receive buffer (remote, or PFT_IPC_STAGED)
+  double* rbuf;                        // its receive buffer
 };
 
 struct pft_slab {
@@ -1672,6 +1702,8 @@ struct pft_slab {
                                  // names the same physical buffer on every slab
   unsigned long long* sig;       // flag words written by the neighbours: [0] from below, [1] from
                                  // above (monotonic exchange sequence numbers); [8] put counter
+  double* rbuf;                  // staged receive buffer (uncached, 2 x 12 planes; pft_slab_ipc_export)
+  int put_role, put_f0, put_f1, put_deep;   // the exchange the last halo_put2 sent (its wait receives it)
   SlabPeer peer[2];              // [0] the neighbour below, [1] above
   int drop_puts;                 // fault injection: halo puts and flag raises skipped (PFT_IPC_DROP_PUTS)
   double* staging;       // host padded layout on the device (for upload/download)
@@ -1915,6 +1947,7 @@ int pft_slab_destroy(pft_slab* s)
   for (int b = 0; b < PFT_BUF_COUNT; ++b)
     if (s->buf0[b]) (void)hipFree(s->buf0[b]);
   if (s->sig) (void)hipFree(s->sig);
+  if (s->rbuf) (void)hipFree(s->rbuf);
   if (s->staging) (void)hipFree(s->staging);
   if (s->noise) (void)hipFree(s->noise);
   for (int st = 0; st < 6; ++st)
@@ -2948,12 +2981,29 @@ int pft_slab_swap_buffers(pft_slab* s, int a, int b)
 
 int pft_slab_accept(pft_slab* s) { return pft_slab_swap_buffers(s, PFT_BUF_X, PFT_BUF_XN); }
 
+static int ensure_rbuf(pft_slab* s)
+{
+  // two slots (exchange sequence number parity): a neighbour can be one exchange ahead -- its
+  // next put needs only our flag of this exchange, which we raise before copying its planes out
+  if (!s->rbuf) HIPCHK(hipExtMallocWithFlags((void**)&s->rbuf, sizeof(double) * 24 * (size_t)s->plane, hipDeviceMallocUncached));
+  return 0;
+}
+
 int pft_slab_ipc_export(pft_slab* s, void* handles)
 {
   hipIpcMemHandle_t* h = (hipIpcMemHandle_t*)handles;
+  int rc = ensure_rbuf(s);
+  if (rc) return rc;
   for (int b = 0; b < PFT_BUF_COUNT; ++b) HIPCHK(hipIpcGetMemHandle(&h[b], s->buf0[b]));
   HIPCHK(hipIpcGetMemHandle(&h[PFT_BUF_COUNT], s->sig));
+  HIPCHK(hipIpcGetMemHandle(&h[PFT_BUF_COUNT + 1], s->rbuf));
   return 0;
+}
+
+static int ipc_staged_env()
+{
+  const char* e = getenv("PFT_IPC_STAGED");
+  return e && atoi(e) == 1;
 }
 
 int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, long fs, int device)
@@ -2964,8 +3014,12 @@ int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, lo
   if (!handles) {
     // self exchange (diagnostic, one slab): the planes land in the slab's own ghost planes, which a
     // single slab never reads (mirror bottom, Dirichlet top)
+    int rc = ensure_rbuf(s);
+    if (rc) return rc;
     for (int b = 0; b < PFT_BUF_COUNT; ++b) p.base[b] = s->buf0[b] + s->plane;
     p.sig = s->sig;
+    p.rbuf = s->rbuf;
+    p.staged = ipc_staged_env();
     p.n3 = s->d.n3;
     p.fs = s->fs;
     p.opened = 0;
@@ -2974,35 +3028,27 @@ int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, lo
   }
   int mine = 0;
   HIPCHK(hipGetDevice(&mine));
-  if (device != mine) {
-    // A neighbour on another GPU writes our ghost planes over xGMI.  Whether this GPU's L2 can
-    // still hold lines of a ghost plane from before that write (coarse-grained hipMalloc memory)
-    // has not been verified on hardware, and a stale line would silently corrupt the halo: refused
-    // unless explicitly enabled (use the RCCL transport across GPUs)
-    const char* e = getenv("PFT_IPC_CROSS_GPU");
-    if (!(e && atoi(e) == 1)) {
-      snprintf(g_err, sizeof(g_err),
-               "ipc neighbour on device %d, this slab on device %d: cross-GPU ipc halos are unverified "
-               "(set PFT_IPC_CROSS_GPU=1 to allow; the rccl transport is the supported one)",
-               device, mine);
-      fprintf(stderr, "libpft: %s\n", g_err);
-      return -2;
-    }
-  }
   const hipIpcMemHandle_t* h = (const hipIpcMemHandle_t*)handles;
-  for (int b = 0; b <= PFT_BUF_COUNT; ++b) {
+  for (int b = 0; b <= PFT_BUF_COUNT + 1; ++b) {
     void* ptr = nullptr;
     const hipError_t e = hipIpcOpenMemHandle(&ptr, h[b], hipIpcMemLazyEnablePeerAccess);
     if (e != hipSuccess) {
-      for (int q = 0; q < b; ++q) (void)hipIpcCloseMemHandle(p.base[q] - s->plane);
+      for (int q = 0; q < b && q < PFT_BUF_COUNT; ++q) (void)hipIpcCloseMemHandle(p.base[q] - s->plane);
+      if (b > PFT_BUF_COUNT) (void)hipIpcCloseMemHandle(p.sig);
       return fail(e, "hipIpcOpenMemHandle");
     }
     if (b < PFT_BUF_COUNT) p.base[b] = (double*)ptr + s->plane;   // the neighbour's buffer pointer
-    else p.sig = (unsigned long long*)ptr;
+    else if (b == PFT_BUF_COUNT) p.sig = (unsigned long long*)ptr;
+    else p.rbuf = (double*)ptr;
   }
   p.n3 = n3;
   p.fs = fs;
   p.remote = device != mine;
+  // A neighbour on another GPU writes into our receive buffer (uncached) rather than our ghost
+  // planes, and we copy it in after the flag wait: no L2 of ours can hold a stale line of what it
+  // wrote.  Both sides take the same decision (remote is symmetric; the env
+  // is the test hook that stages between processes on one GPU).
+  p.staged = p.remote || ipc_staged_env();
   p.opened = 1;
   p.on = 1;
   return 0;
@@ -3015,6 +3061,7 @@ int pft_slab_ipc_close(pft_slab* s)
     if (p.on && p.opened) {
       for (int b = 0; b < PFT_BUF_COUNT; ++b) (void)hipIpcCloseMemHandle(p.base[b] - s->plane);
       (void)hipIpcCloseMemHandle(p.sig);
+      (void)hipIpcCloseMemHandle(p.rbuf);
     }
     memset(&p, 0, sizeof(p));
   }
@@ -3035,6 +3082,10 @@ double* pft_slab_far(pft_slab* s, int which, int q, int side)
 int pft_slab_halo_put2(pft_slab* s, int role, int f0, int f1, int deep, unsigned long long seq)
 {
   if (role < 0 || role >= PFT_BUF_COUNT || f0 < 0 || f1 > 3 || f1 <= f0) return -2;
+  s->put_role = role;
+  s->put_f0 = f0;
+  s->put_f1 = f1;
+  s->put_deep = deep ? 1 : 0;
   if (s->drop_puts) return 0;
   const int ph = s->phys[role];
   PutArgs a;
@@ -3045,20 +3096,25 @@ int pft_slab_halo_put2(pft_slab* s, int role, int f0, int f1, int deep, unsigned
   a.n3 = s->d.n3;
   a.f0 = f0;
   a.nf = f1 - f0;
+  // staged: into the neighbour's receive buffer [side][depth][field][plane] -- the neighbour below
+  // receives our planes as "from above" (side 1), the one above as "from below" (side 0)
+  const long P = s->plane;
+  const long slot = (long)(seq & 1) * 12 * P;   // the receive-buffer slot of this exchange
   if (s->peer[0].on) {
-    a.dlo = s->peer[0].base[ph] + (long)(s->peer[0].n3 + 1) * s->plane;
-    a.dlo_fs = s->peer[0].fs;
+    a.dlo = s->peer[0].staged ? s->peer[0].rbuf + slot + (1 * 2 + 0) * 3 * P : s->peer[0].base[ph] + (long)(s->peer[0].n3 + 1) * P;
+    a.dlo_fs = s->peer[0].staged ? P : s->peer[0].fs;
   }
   if (s->peer[1].on) {
-    a.dhi = s->peer[1].base[ph];
-    a.dhi_fs = s->peer[1].fs;
+    a.dhi = s->peer[1].staged ? s->peer[1].rbuf + slot + (0 * 2 + 0) * 3 * P : s->peer[1].base[ph];
+    a.dhi_fs = s->peer[1].staged ? P : s->peer[1].fs;
   }
   if (!a.dlo && !a.dhi) return 0;
   if (deep) {
     // the second boundary planes into the neighbours' far ghost planes (pft_slab_far layout)
     a.deep = 1;
-    if (s->peer[0].on) a.flo = s->peer[0].base[ph] + (long)(s->peer[0].n3 + 2) * s->plane;
-    if (s->peer[1].on) a.fhi = s->peer[1].base[ph] - (long)s->plane;
+    if (s->peer[0].on)
+      a.flo = s->peer[0].staged ? s->peer[0].rbuf + slot + (1 * 2 + 1) * 3 * P : s->peer[0].base[ph] + (long)(s->peer[0].n3 + 2) * P;
+    if (s->peer[1].on) a.fhi = s->peer[1].staged ? s->peer[1].rbuf + slot + (0 * 2 + 1) * 3 * P : s->peer[1].base[ph] - P;
   }
   const long n = (deep ? 4L : 2L) * a.nf * s->plane;
   const int blocks = (int)std::min<long>(1024, std::max<long>(1, (n + 255) / 256));
@@ -3073,7 +3129,8 @@ int pft_slab_halo_signal(pft_slab* s, unsigned long long seq)
   unsigned long long* slo = s->peer[0].on ? s->peer[0].sig + 1 : nullptr;   // below: its "from above"
   unsigned long long* shi = s->peer[1].on ? s->peer[1].sig + 0 : nullptr;   // above: its "from below"
   if (!slo && !shi) return 0;
-  halo_signal_kernel<<<1, 64, 0, s->stream>>>(slo, shi, seq, s->peer[0].remote || s->peer[1].remote);
+  halo_signal_kernel<<<1, 64, 0, s->stream>>>(slo, shi, seq,
+                                              s->peer[0].remote || s->peer[1].remote || s->peer[0].staged || s->peer[1].staged);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -3081,8 +3138,30 @@ int pft_slab_halo_signal(pft_slab* s, unsigned long long seq)
 int pft_slab_halo_wait(pft_slab* s, unsigned long long seq)
 {
   // flags [0] (from below) and [1] (from above): the stream goes on once both planes are in
-  for (int side = 0; side < 2; ++side)
-    if (s->peer[side].on) HIPCHK(hipStreamWaitValue64(s->stream, s->sig + side, seq, hipStreamWaitValueGte, ~0ULL));
+  int sides = 0;
+  for (int side = 0; side < 2; ++side) {
+    if (!s->peer[side].on) continue;
+    HIPCHK(hipStreamWaitValue64(s->stream, s->sig + side, seq, hipStreamWaitValueGte, ~0ULL));
+    if (s->peer[side].staged) sides |= 1 << side;
+  }
+  if (sides) {
+    // staged: what the neighbours put into the receive buffer, into the ghost planes of the
+    // exchange's buffer (the one the last halo_put2 sent: every rank runs the same sequence)
+    RecvArgs r;
+    r.rbuf = s->rbuf + (long)(seq & 1) * 12 * s->plane;
+    r.dst = s->buf[s->put_role];
+    r.fs = s->fs;
+    r.plane = s->plane;
+    r.n3 = s->d.n3;
+    r.f0 = s->put_f0;
+    r.nf = s->put_f1 - s->put_f0;
+    r.depth = s->put_deep ? 2 : 1;
+    r.sides = sides;
+    const long n = 4L * r.nf * s->plane;
+    const int blocks = (int)std::min<long>(1024, std::max<long>(1, (n + 255) / 256));
+    halo_recv_kernel<<<blocks, 256, 0, s->stream>>>(r);
+    HIPCHK(hipGetLastError());
+  }
   return 0;
 }
 

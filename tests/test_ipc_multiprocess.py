@@ -115,11 +115,55 @@ def test_400_processes_equal_one_slab(tmp_path, nranks):
     assert np.array_equal(np.concatenate([r["states"][0] for r in res], axis=1), x)
 
 
+@pytest.mark.parametrize("nranks,pair", [(2, 0), (3, 2)])
+def test_g20_processes_staged_receive_equal_reference(tmp_path, nranks, pair):
+    """the staged receive a neighbour on another GPU gets (here forced between processes on one
+    GPU, PFT_IPC_STAGED=1): planes into the receiver's uncached receive buffer, copied into its
+    ghost (and far ghost) planes after the flag wait -- golden g20 bit for bit, one launch per
+    stage and pair kernels (two-plane halo)"""
+    meta, A = O.load_case("g20")
+    times = meta["traj_times"][:2]
+    env = {r: {"PFT_IPC_STAGED": "1"} for r in range(nranks)}
+    res = _run_ranks(tmp_path, nranks, rank_env=env, case="g20", times=times, tile=2, pair=pair)
+    for r in res:
+        assert int(r["path"]) == 1 and int(r["pairs"]) == (1 if pair else 0)
+    for i in range(len(times)):
+        ref = meta["traj_m0"][i]
+        for r in res:
+            t, h, s, st, rc = r["rows"][i]
+            assert (t.hex(), h.hex(), int(s), int(st), int(rc)) == \
+                (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(), ref[2], ref[3], ref[4])
+        full = np.concatenate([r["states"][i] for r in res], axis=1)
+        assert np.array_equal(full, A[f"traj_m0_state{i}"])
+
+
+def test_400_processes_staged_receive_equal_one_slab(tmp_path):
+    """400^3 over 2 processes with the pair kernels and the staged receive (PFT_IPC_STAGED=1)"""
+    steps = 8
+    base, Pm, info = M.full_size_case(400, 0)
+    sim = P.Simulation(info["n1"], info["n2"], info["n3"], (info["L1"], info["L2"], info["L3"]), 0, Pm,
+                       beads=O.beads(), tau=1.0, tau_min=info["tau_min"], delta=info["delta"])
+    assert sim.solve_ex(1e9, steps, 0) == 2
+    got = (sim.t, sim.h, sim.system.steps, sim.system.steps_total)
+    x = sim.interior()
+    sim.close()
+    env = {r: {"PFT_IPC_STAGED": "1"} for r in range(2)}
+    res = _run_ranks(tmp_path, 2, rank_env=env, case="default", grid_nodes=400, times=[1e9], steps=steps, pair=2)
+    for r in res:
+        assert int(r["pairs"]) == 1
+        t, h, s, st, rc = r["rows"][0]
+        assert (t, h, int(s), int(st), int(rc)) == got + (2,)
+    assert np.array_equal(np.concatenate([r["states"][0] for r in res], axis=1), x)
+
+
+@pytest.mark.parametrize("staged", [0, 1])
 @pytest.mark.parametrize("tile", [None, 32])
-def test_ipc_self_exchange_equals_reference(tile):
+def test_ipc_self_exchange_equals_reference(tile, staged, monkeypatch):
     """one process, ipc communicator of size 1 exchanging with itself: the put kernel, the flag
     words and the stream waits of every stage run; the planes land in ghost planes one slab never
     reads, so the trajectory is the reference's"""
+    if staged:
+        monkeypatch.setenv("PFT_IPC_STAGED", "1")      # the receive-buffer path (read at set_peer)
     meta, A = O.load_case("g20")
     Pm, info = O.params_from_meta(meta)
     comm = P.comm_init_ipc(1, 0, f"/pft_selfx_{os.getpid()}_{uuid.uuid4().hex[:12]}")
