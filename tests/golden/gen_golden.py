@@ -22,6 +22,8 @@ Cases (SURVEY.md section 4.2 KATs 1-4):
   g100     BASELINE configs[0]: default Params at grid_nodes 100 (50x50x100): parameters, the
            SHA-256 of the IC and of a mode-0 trajectory to two snapshot times (checked identical
            on 2 ranks), plus the middle and top z-planes of each state (a state is 6 MB).
+  g20nf    the g20 trajectory record for calc_mode 10 and 11 (to t = 36, 360, 720 s), checked
+           identical on 3 ranks.
   g200     BASELINE configs[1]: grid_nodes 200 (100x100x200), the same record for calc_mode 0 to
            t = 0.01 and 0.03 s (35 and 65 attempted steps) and calc_mode 1 to t = 0.03 s; run on
            8 MPI ranks and checked identical on 3.
@@ -168,6 +170,38 @@ def case_g20():
                 wm.close()
     finally:
         w.close()
+    return arrays, meta
+
+
+def case_g20nf():
+    """g20's trajectory record for the two remaining models, calc_mode 10 and 11 (the RHS without
+    the heat-flux term, equation.c:650-731 with du = 0), from the default IC to the same snapshot
+    times, checked identical on 3 ranks"""
+    arrays, meta = {}, {"case": "g20nf", "source": "reference Params, grid_nodes 20, calc_mode 10 and 11"}
+    times = [36.0, 360.0, 720.0]
+    meta["traj_times"] = times
+    for mode in (10, 11):
+        wm = Work({"grid_nodes": 20, "calc_mode": mode})
+        try:
+            o = wm.run(1, "setup")
+            p = read_params(o)
+            shape = (3, p["n3"], p["n2"], p["n1"])
+            ic_m = load(os.path.join(o, "ic.f64"), shape)
+            icp = os.path.join(wm.dir, "icm.f64")
+            ic_m.tofile(icp)
+            o1 = wm.run(1, "solve", icp, 0.0, 1.0, *times)
+            tm, st = traj(o1, len(times), shape)
+            o3 = wm.run(3, "solve", icp, 0.0, 1.0, *times)
+            tm3, st3 = traj(o3, len(times), shape)
+            assert tm == tm3 and all(np.array_equal(a, b) for a, b in zip(st, st3)), \
+                f"decomposition invariance broken for mode {mode}"
+            arrays[f"traj_m{mode}_ic"] = ic_m
+            for i, x in enumerate(st):
+                arrays[f"traj_m{mode}_state{i}"] = x
+            meta[f"traj_m{mode}"] = tm
+            meta[f"m{mode}_params"] = hexify(p)
+        finally:
+            wm.close()
     return arrays, meta
 
 
@@ -364,7 +398,7 @@ def main():
     if not os.path.exists(PFT_REF):
         sys.exit("build the reference harness first: make -C oracle ref")
     cases = {"g20": case_g20, "ragged": case_ragged, "g100": case_g100, "ctl": case_ctl, "g200": case_g200,
-             "g400": case_g400}
+             "g400": case_g400, "g20nf": case_g20nf}
     for name in sys.argv[1:] or list(cases):
         arrays, meta = cases[name]()
         name = meta["case"]

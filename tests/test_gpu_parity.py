@@ -76,6 +76,30 @@ def test_trajectory_bitwise(mode, gl_static, flavour):
     sim.close()
 
 
+@pytest.mark.parametrize("mode", [10, 11])
+@pytest.mark.parametrize("flavour", sorted(FLAVOURS) + ["pairs"])
+def test_trajectory_no_flux_modes_bitwise(mode, flavour):
+    """calc_mode 10 and 11 on the device to the g20 snapshot times: the reference's own trajectory
+    (tests/golden/g20nf) bit for bit, every kernel flavour and the pair kernels forced"""
+    meta, A = O.load_case("g20nf")
+    m = {"params": meta[f"m{mode}_params"]}
+    pair = flavour == "pairs"
+    P.lib().pft_solver_set_option(P.PFT_OPT_PAIR, 2 if pair else 1)
+    try:
+        sim, Pm, info = make_sim(m, A[f"traj_m{mode}_ic"], mode=mode, flavour="fusedauto" if pair else flavour)
+        for i, T in enumerate(meta["traj_times"]):
+            rc = sim.solve(T)
+            ref = meta[f"traj_m{mode}"][i]
+            assert (sim.t.hex(), sim.h.hex(), sim.system.steps, sim.system.steps_total, rc) == \
+                (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(), ref[2], ref[3], ref[4])
+            assert np.array_equal(sim.interior(), A[f"traj_m{mode}_state{i}"])
+        st = sim.stats()
+        assert st.path == 1 and bool(st.pairs) == pair
+        sim.close()
+    finally:
+        P.lib().pft_solver_set_option(P.PFT_OPT_PAIR, 1)
+
+
 def test_trajectory_mode2_tolerance():
     meta, A = O.load_case("g20")
     sim, Pm, info = make_sim(meta, A["traj_m2_ic"], mode=2)

@@ -96,3 +96,18 @@ def test_single_step_bitwise(ragged, tag):
     r = m["result"]
     assert (t.hex(), h.hex(), s, st, rc) == (float.fromhex(r[0]).hex(), float.fromhex(r[1]).hex(), r[2], r[3], r[4])
     assert np.array_equal(x, A[f"step_{tag}"])
+
+
+@pytest.mark.parametrize("mode", [10, 11])
+def test_trajectory_no_flux_modes_bitwise(mode):
+    """calc_mode 10 and 11 (no heat-flux term, du = 0): the oracle's trajectory to the g20 snapshot
+    times equals the reference's own (tests/golden/g20nf, from gen_golden.py)"""
+    meta, A = O.load_case("g20nf")
+    P, info = O.params_from_meta({"params": meta[f"m{mode}_params"]})
+    assert info["calc_mode"] == mode
+    res = O.solve(info, P, mode, A[f"traj_m{mode}_ic"], 0.0, 1.0, meta["traj_times"])
+    for i, (t, h, s, st, rc, x) in enumerate(res):
+        ref = meta[f"traj_m{mode}"][i]
+        assert (t.hex(), h.hex(), s, st, rc) == (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(),
+                                                 ref[2], ref[3], ref[4])
+        assert np.array_equal(x, A[f"traj_m{mode}_state{i}"])
