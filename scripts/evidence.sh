@@ -28,6 +28,8 @@ timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $O/prof/fetch -o run --output-fo
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $O/prof/write -o run --output-format csv -- python3 bench.py $ARGS > $O/prof/write_bench.json 2> $O/prof/write.err; fatal $? write
 timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE -d $O/prof/valu -o run --output-format csv -- python3 bench.py $ARGS > $O/prof/valu_bench.json 2> $O/prof/valu.err; fatal $? valu
 timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 GRBM_GUI_ACTIVE -d $O/prof/fp64 -o run --output-format csv -- python3 bench.py $ARGS > $O/prof/fp64_bench.json 2> $O/prof/fp64.err; fatal $? fp64
+# L2 hits and misses per kernel (pair 4+5's re-loaded operands)
+timeout -s KILL 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum -d $O/prof/tcc -o run --output-format csv -- python3 bench.py $ARGS > $O/prof/tcc_bench.json 2> $O/prof/tcc.err; fatal $? tcc
 PB=$(python3 -c "import json;print(json.load(open('$O/prof/trace_bench.json'))['probe_bytes_each_way'])")
 python3 scripts/pmc_summary.py $O/prof/trace $O/prof/fetch $O/prof/write 200x200x400 $PB $O/pmc_summary.json $O/prof/valu $O/prof/fp64 > $O/pmc_summary.txt 2>&1; fatal $? pmc_summary
 cp $O/pmc_summary.json profiles/pmc_summary.json
