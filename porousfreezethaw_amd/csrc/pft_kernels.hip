@@ -1706,6 +1706,10 @@ struct pft_slab {
   int put_role, put_f0, put_f1, put_deep;   // the exchange the last halo_put2 sent (its wait receives it)
   SlabPeer peer[2];              // [0] the neighbour below, [1] above
   int drop_puts;                 // fault injection: halo puts and flag raises skipped (PFT_IPC_DROP_PUTS)
+  int ipc_poisoned;              // an ipc wait timed out: the flag words were forced past every
+                                 // sequence number, so no later halo wait would block -- every halo
+                                 // exchange, wait and sync refuses (PFT_ERR_IPC_TIMEOUT) until
+                                 // pft_slab_ipc_close resets the flags (a detach / re-attach)
   double* staging;       // host padded layout on the device (for upload/download)
   long S;                // host padded block (one field)
   unsigned long long* scratch;  // [0] eps bits, [1] nonfinite flag
@@ -1791,9 +1795,16 @@ static double wall_s()
 // s->timeout_s the slab raises its own flag words past every sequence number (on the side stream,
 // which nothing blocks): the compute stream drains -- its results are void -- and the caller gets
 // PFT_ERR_IPC_TIMEOUT, which RK_MPI_SA_solve reports as PFT_SOLVE_DEVICE_ERROR.
+static int slab_poisoned(pft_slab* s, const char* what)
+{
+  snprintf(g_err, sizeof(g_err), "%s: an earlier ipc halo wait timed out; detach and re-attach the slab", what);
+  return PFT_ERR_IPC_TIMEOUT;
+}
+
 static int slab_timed_out(pft_slab* s, const char* what)
 {
   static const unsigned long long released[2] = {~0ULL >> 1, ~0ULL >> 1};
+  s->ipc_poisoned = 1;
   (void)hipMemcpyAsync(s->sig, released, sizeof(released), hipMemcpyHostToDevice, s->side);
   (void)hipStreamSynchronize(s->side);
   (void)hipStreamSynchronize(s->stream);
@@ -1808,6 +1819,12 @@ static int slab_timed_out(pft_slab* s, const char* what)
 // peer, bounded by s->timeout_s with one
 static int slab_wait(pft_slab* s, hipEvent_t ev, const char* what)
 {
+  if (s->ipc_poisoned) {
+    // the released flags let the stream drain: wait for it, then refuse
+    (void)hipStreamSynchronize(s->stream);
+    (void)hipGetLastError();
+    return slab_poisoned(s, what);
+  }
   if (!s->peer[0].on && !s->peer[1].on) {
     HIPCHK(ev ? hipEventSynchronize(ev) : hipStreamSynchronize(s->stream));
     return 0;
@@ -2539,6 +2556,7 @@ int pft_slab_eps_mark_on(pft_slab* s, void* stream)
 
 int pft_slab_eps_fetch(pft_slab* s, double* eps, int* nonfinite)
 {
+  if (s->ipc_poisoned) return slab_poisoned(s, "pft_slab_eps_fetch");
   if (s->eps_marked == 2) {
     // published beside the speculative stage 1 (deferred publication): poll the slot (pinned,
     // coherent) until both words left the sentinel while that kernel keeps running.  Without a
@@ -3056,6 +3074,15 @@ int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, lo
 
 int pft_slab_ipc_close(pft_slab* s)
 {
+  if (s->ipc_poisoned) {
+    // the flags were forced past every sequence number: back to 0 for the next attach (the compute
+    // stream has drained, slab_wait)
+    (void)hipStreamSynchronize(s->stream);
+    (void)hipStreamSynchronize(s->side);
+    HIPCHK(hipMemset(s->sig, 0, 2 * sizeof(unsigned long long)));
+    HIPCHK(hipDeviceSynchronize());
+    s->ipc_poisoned = 0;
+  }
   for (int side = 0; side < 2; ++side) {
     SlabPeer& p = s->peer[side];
     if (p.on && p.opened) {
@@ -3082,6 +3109,7 @@ double* pft_slab_far(pft_slab* s, int which, int q, int side)
 int pft_slab_halo_put2(pft_slab* s, int role, int f0, int f1, int deep, unsigned long long seq)
 {
   if (role < 0 || role >= PFT_BUF_COUNT || f0 < 0 || f1 > 3 || f1 <= f0) return -2;
+  if (s->ipc_poisoned) return slab_poisoned(s, "pft_slab_halo_put2");
   s->put_role = role;
   s->put_f0 = f0;
   s->put_f1 = f1;
@@ -3125,6 +3153,7 @@ int pft_slab_halo_put2(pft_slab* s, int role, int f0, int f1, int deep, unsigned
 
 int pft_slab_halo_signal(pft_slab* s, unsigned long long seq)
 {
+  if (s->ipc_poisoned) return slab_poisoned(s, "pft_slab_halo_signal");
   if (s->drop_puts) return 0;
   unsigned long long* slo = s->peer[0].on ? s->peer[0].sig + 1 : nullptr;   // below: its "from above"
   unsigned long long* shi = s->peer[1].on ? s->peer[1].sig + 0 : nullptr;   // above: its "from below"
@@ -3138,6 +3167,7 @@ int pft_slab_halo_signal(pft_slab* s, unsigned long long seq)
 int pft_slab_halo_wait(pft_slab* s, unsigned long long seq)
 {
   // flags [0] (from below) and [1] (from above): the stream goes on once both planes are in
+  if (s->ipc_poisoned) return slab_poisoned(s, "pft_slab_halo_wait");
   int sides = 0;
   for (int side = 0; side < 2; ++side) {
     if (!s->peer[side].on) continue;

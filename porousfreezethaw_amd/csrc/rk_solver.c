@@ -52,6 +52,8 @@ typedef struct {
 	double k1_t;
 	pft_consts k1_c;
 	pft_slab * k1_slab;
+	int k1_deep;                /* ... and its far ghost planes are current: the call that left it ran
+	                               the deep (pair, between slabs) exchange, not one launch per stage */
 	int deep;                   /* this call runs the pair kernels on z-neighbouring slabs: every stage
 	                               launch covers the whole slab and is followed by the two-plane halo
 	                               exchange of its output (pft_comm_halo_deep) */
@@ -409,11 +411,13 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 	R.deep = pair && pft_comm_splits(c);
 	{
 		/* K1 from the previous call (R.k1_keep): x resident and unchanged since (no upload), the
-		   same slab, t, constants, and no u_noise (re-uploaded every call).  Every rank takes the
-		   same decision (the same calls, flags and t). */
+		   same slab, t, constants, and no u_noise (re-uploaded every call); for the pair kernels
+		   between slabs also its far ghost planes (R.k1_deep: a call with one launch per stage
+		   exchanged only the first ghost plane, and the deep prologue below re-exchanges only X
+		   and XN).  Every rank takes the same decision (the same calls, flags and t). */
 		pft_consts cc;
 		if(spec && (flags & PFT_SOLVE_REUSE_DEVICE) && R.device_valid && R.k1_keep && R.k1_slab == R.slab &&
-		   !pft_model_noise() && memcmp(&R.k1_t, &t, sizeof t) == 0 && !pft_model_get_consts(&cc) &&
+		   (!R.deep || R.k1_deep) && !pft_model_noise() && memcmp(&R.k1_t, &t, sizeof t) == 0 && !pft_model_get_consts(&cc) &&
 		   memcmp(&cc, &R.k1_c, sizeof cc) == 0)
 			k1_valid = 1;
 		R.k1_keep = 0;
@@ -650,6 +654,7 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 		R.k1_keep = 1;
 		R.k1_t = t;
 		R.k1_slab = R.slab;
+		R.k1_deep = R.deep;
 	}
 	if(R.opt_timing) pft_slab_timing_flush(R.slab, R.stats.stage_ms, R.stats.stage_n);
 	R.tstep = 0;

@@ -190,10 +190,17 @@ def test_lost_ipc_halo_ends_in_device_error_not_a_hang(tmp_path):
     host wait of the slab is bounded by PFT_IPC_TIMEOUT (here 5 s): both ranks return
     PFT_SOLVE_DEVICE_ERROR and exit, with the raw status an ipc timeout (-5000 host round,
     -5002 device halo) -- not a hang"""
-    res = _run_ranks(tmp_path, 2, timeout=180, case="g20", times=[36.0], raw_rc=True, ipc_timeout="5",
-                     rank_env={1: {"PFT_IPC_DROP_PUTS": "1"}})
+    res = _run_ranks(tmp_path, 2, timeout=240, case="g20", times=[36.0], raw_rc=True, ipc_timeout="5",
+                     second_call=True, rank_env={1: {"PFT_IPC_DROP_PUTS": "1"}})
     for r in res:
         assert int(r["rc"]) == P.PFT_SOLVE_DEVICE_ERROR
         assert int(r["status"]) in (-5000, -5002)
         assert float(r["seconds"]) < 60
     assert int(res[0]["status"]) == -5002            # rank 0 waited on the device flag
+    # a second solve on the same comm and slab (ADVICE r03): the timed-out slab's flag words were
+    # forced past every sequence number, so without the refusal its halo waits would all pass and
+    # it would run on stale ghost planes; it must fail again, within the bound
+    for r in res:
+        assert int(r["rc2"]) == P.PFT_SOLVE_DEVICE_ERROR
+        assert int(r["status2"]) in (-5000, -5002)
+        assert float(r["seconds2"]) < 60

@@ -216,6 +216,55 @@ def test_pair_multislab_loopback_equals_one_slab(nprocs, dims):
     assert np.array_equal(np.concatenate([o[0][0][5] for o in out], axis=1), ref[4])
 
 
+def test_pair_multislab_k1_carried_from_stage_launch_call():
+    """a resident call with one launch per stage (PFT_OPT_PAIR 0: K1's first ghost plane
+    only) followed by a REUSE_DEVICE call with the pair kernels between slabs, whose stage A reads
+    K1's far ghost planes: the carried K1 must not be used there (R.k1_deep), so the two calls
+    equal 10 continuous single-slab pair steps bit for bit"""
+    dims, nprocs = (30, 30, 60), 3
+    ref, used, *_ = _run(dims, 0, True, 10)
+    meta, _ = O.load_case("g20")
+    L = P.lib()
+    group = C.c_void_p()
+    assert L.pft_comm_init_loopback(C.byref(group), nprocs) == 0
+    out, errs = [None] * nprocs, []
+
+    def worker(r):
+        try:
+            mine = C.c_void_p()
+            assert L.pft_comm_loopback_rank(group, r, C.byref(mine)) == 0
+            L.pft_comm_set_current(mine)
+            Pm, info = O.params_from_meta(meta)
+            sim = P.Simulation(*dims, (info["L1"], info["L2"], info["L3"]), 0, Pm, nprocs=nprocs, rank=r,
+                               beads=O.beads(), tau=1.0, tau_min=info["tau_min"], delta=info["delta"], tile=2)
+            L.pft_solver_set_option(P.PFT_OPT_PAIR, 0)          # per host thread
+            assert sim.solve_ex(1e9, 5, P.PFT_SOLVE_KEEP_DEVICE) == 2
+            p0 = sim.stats().pairs
+            L.pft_solver_set_option(P.PFT_OPT_PAIR, 2)
+            assert sim.solve_ex(1e9, 5, P.PFT_SOLVE_REUSE_DEVICE) == 2
+            out[r] = (sim.t.hex(), sim.h.hex(), sim.system.steps, sim.system.steps_total, sim.interior(),
+                      p0, sim.stats().pairs)
+            sim.close()
+            L.pft_solver_set_option(P.PFT_OPT_PAIR, 1)
+            L.pft_comm_set_current(None)
+            L.pft_comm_destroy(mine)
+        except BaseException as e:   # noqa: BLE001 -- surfaced below
+            errs.append(e)
+
+    ths = [threading.Thread(target=worker, args=(r,)) for r in range(nprocs)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=600)
+    L.pft_comm_destroy(group)
+    if errs:
+        raise errs[0]
+    assert used == 1 and all(o[5] == 0 and o[6] == 1 for o in out)
+    for o in out:
+        assert o[:4] == ref[:4]
+    assert np.array_equal(np.concatenate([o[4] for o in out], axis=1), ref[4])
+
+
 @pytest.mark.parametrize("transport", ["rccl", "ipc"])
 def test_pair_self_exchange(transport):
     """one slab, a 1-rank communicator exchanging with itself: the two-plane halo of every launch
