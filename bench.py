@@ -84,6 +84,8 @@ def parse():
     ap.add_argument("--no-recompute", action="store_true",
                     help="materialise the reference's aux arrays between stages (72 vs 54 doubles/cell-step)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--host-ic", action="store_true",
+                    help="initial condition on the host (default: on the device, bit-identical, f1)")
     ap.add_argument("--gate", type=int, default=0, choices=(0, 1),
                     help="gated steps on small single slabs (PFT_OPT_GATE, f4; default off: measured neutral)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
@@ -168,7 +170,7 @@ def main():
     sim = P.Simulation(n1, n2, total_n3, Ls, a.mode, prm, nprocs=world, rank=rank, beads=beads,
                        tau=base["tau"], tau_min=base["tau_min"], delta=base["delta"],
                        gl_static=a.gl_static, kz=a.kz or None, tile=a.tile,
-                       recompute=not a.no_recompute)
+                       recompute=not a.no_recompute, device_ic=not a.host_ic)
     init_s = time.time() - t0
     cells_rank = n1 * n2 * sim.grid.n3
     cells_total = n1 * n2 * total_n3
@@ -344,6 +346,7 @@ def main():
         # with one launch per stage), per GPU
         "step_algorithmic_GBps": round(step_bytes * cells_total * steps / el / 1e9 / world, 1),
         "init_s": round(init_s, 2),
+        "initial_condition": "host" if a.host_ic else "device",
     }
 
     if a.probe:
@@ -436,7 +439,7 @@ def parity_check(ranks, calls, a, base, dims, Ls, beads, final_time, dev):
     L.pft_hip_set_device(dev)
     ref = P.Simulation(n1, n2, total_n3, Ls, a.mode, P.params_array(base), nprocs=1, rank=0, beads=beads,
                        tau=base["tau"], tau_min=base["tau_min"], delta=base["delta"], gl_static=a.gl_static,
-                       kz=a.kz or None, tile=a.tile, recompute=not a.no_recompute)
+                       kz=a.kz or None, tile=a.tile, recompute=not a.no_recompute, device_ic=not a.host_ic)
     for i, k in enumerate(calls):
         flags = P.PFT_SOLVE_KEEP_DEVICE | (P.PFT_SOLVE_REUSE_DEVICE if i else 0)
         rc = ref.solve_ex(final_time, k, flags)

@@ -133,6 +133,28 @@ int pft_slab_set_eps_mult(pft_slab * s, const double * em3);
 /* u_noise field (PrecalculateData, equation.c:450-456), n3*n1*n2 doubles [k][j][i]; NULL clears */
 int pft_slab_set_noise(pft_slab * s, const double * host_noise);
 
+/* f1: the default Params' initial condition and the glass beads (intertrack.c:1880-2010 with
+   Params:9-21; PrecalculateData, equation.c:459-530) evaluated on the device straight into X and
+   XN, bit for bit the host's (pft_model_ic_default + PrecalculateData).  Every term that depends
+   on one coordinate only (the walls' tanh, the (x-L1/2)^2 of the ice disc, the node coordinates)
+   comes in per-axis tables the host evaluates with the C library; the beads' tanh runs on the
+   device as the C library's algorithm (pft_tanh.h).  Tables: [n1] x terms, [n2] y terms, [n3]
+   z terms of this slab's planes; beads: 3*nbeads scaled centres, plane_off[n3+1] / plane_beads[]
+   the candidate beads of each plane (any superset of the beads whose tanh argument is below 22).
+   *gl_unclean: 1 if a gl value is -0.0 or NaN (pft_slab_set_gl_keep). */
+typedef struct {
+	int n1, n2, n3;
+	const double *tx1, *tx2, *px2, *xb;   /* gl wall terms x - L1 + off_x, off_x - x; (x - L1/2)^2; bead x */
+	const double *ty1, *ty2, *py2, *yb;
+	const double *tz1, *tz2, *pz, *zb;    /* gl terms z - 0.055, off_z - z; ice-disc z window (0/1); bead z */
+	double u0, r2;                        /* 293.15 (float_val), (L1/3)^2 */
+	int nbeads;                           /* 0: no bead overlay */
+	const double * bxyz;
+	const int *plane_off, *plane_beads;
+	double s, R, reach2;                  /* 0.5/xi_gl, ball_radius, the host's cull distance^2 */
+} pft_ic_tables;
+int pft_slab_ic_default(pft_slab * s, const pft_ic_tables * t, int * gl_unclean);
+
 /* error norm of the last stage 5: reset before the step, fetch after (blocks on the stream) */
 int pft_slab_eps_reset(pft_slab * s);
 int pft_slab_eps_fetch(pft_slab * s, double * eps, int * nonfinite);

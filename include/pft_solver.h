@@ -31,6 +31,15 @@ int pft_solve_ex(FLOAT final_time, RK_MPI_S_SOLUTION * system, long max_steps_to
    reads only t and h. */
 int pft_solver_download(RK_MPI_S_SOLUTION * system);
 
+/* f1 (after RK_MPI_SA_init): the default Params' initial condition (Params:9-21,
+   intertrack.c:1880-2010) and, with with_beads, the glass beads (PrecalculateData,
+   equation.c:459-530) computed on the device straight into the solver's state, bit for bit what
+   pft_model_ic_default + PrecalculateData give on the host; system->x is not written (download it
+   with pft_solver_download).  The next pft_solve_ex(..., PFT_SOLVE_REUSE_DEVICE) starts from it.
+   Collective when the communicator has several ranks.  0, -3 (no RK_MPI_SA_init), -1 (beads
+   requested but none set) or PFT_SOLVE_DEVICE_ERROR. */
+int pft_solver_ic_default_device(int with_beads);
+
 /* RK_MPI_SA_solve / pft_solve_ex return value added to the reference's codes
    (RK_MPI_SAsolver.h:384-392): a HIP or RCCL failure (out of device memory, a device fault, a
    lost peer).  pft_solver_last_status() gives the raw status (-1000 - hipError_t, -3000 -

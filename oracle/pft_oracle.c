@@ -224,12 +224,17 @@ typedef struct { const pft_or_grid * g; dims d; } rows_t;
 		} \
 	} } while(0)
 
+/* the u_noise field the solve's RHS adds (equation.c:450-456, 676-687); NULL: u_noise_amp == 0 */
+static const double * or_noise = NULL;
+
+void pft_or_set_noise(const double * noise) { or_noise = noise; }
+
 static void rhs_stage(const pft_or_grid * g, const double * P, int cm, double t, double * w,
                       double * dw, pft_or_exchange_fn ex, void * user)
 {
 	pft_or_bcond(g, P, t, w);
 	if(ex) ex(w, user);
-	pft_or_stencil(g, P, cm, w, NULL, dw);
+	pft_or_stencil(g, P, cm, w, or_noise, dw);
 }
 
 static double eps_max(const rows_t * R, const double * K1, const double * K3, const double * K4,

@@ -43,6 +43,10 @@ void pft_or_stencil(const pft_or_grid * g, const double * param, int calc_mode,
                     const double * w, const double * noise, double * dw);
 /* PrecalculateData constants (equation.c:442-447) are derived inside pft_or_stencil */
 
+/* the u_noise field ([k][j][i] of the slab, equation.c:450-456) that pft_or_solve's right-hand
+   side adds (equation.c:676-687); NULL (the default) for u_noise_amp == 0.  Single slab only. */
+void pft_or_set_noise(const double * noise);
+
 /* full single-slab RHS: bcond + stencil */
 void pft_or_rhs(const pft_or_grid * g, const double * param, int calc_mode, double t,
                 double * w, double * dw);

@@ -20,7 +20,9 @@
  *        (glass beads) -> <outdir>/params.txt, <outdir>/ic.f64 (global interior [q][k][j][i])
  *   pft_ref rhs   <Params> <outdir> <state.f64> <t>
  *        K = f(t, state) through the reference meta-pointer -> <outdir>/rhs.f64 (interior),
- *        <outdir>/w_rank<r>.f64 (each rank's full padded input array after bcond+sync)
+ *        <outdir>/w_rank<r>.f64 (each rank's full padded input array after bcond+sync),
+ *        <outdir>/noise_rank<r>.f64 (each rank's u_noise field, equation.c:450-456, [k][j][i];
+ *        rand() is not seeded here, so it is glibc's sequence from seed 1)
  *   pft_ref solve <Params> <outdir> <state.f64> <t0> <h0> <T1> [<T2> ...]
  *        RK_MPI_SA_solve() to each T_i in turn (like intertrack.c:2283) -> <outdir>/traj.txt
  *        (t, h, steps, steps_total, return code per call, hex floats) and
@@ -316,6 +318,13 @@ int main(int argc, char ** argv)
 		sprintf(path, "%s/rhs.f64", argv[3]); gather_write(K, path);
 		sprintf(path, "%s/w_rank%d.f64", argv[3], MPIrank);
 		{ FILE * f = fopen(path, "wb"); fwrite(solution, sizeof(FLOAT), VAR_COUNT*subgridSIZE, f); fclose(f); }
+		sprintf(path, "%s/noise_rank%d.f64", argv[3], MPIrank);
+		{
+			FILE * f = fopen(path, "wb");
+			int i;
+			for(i=0;i<n1*n2*n3;i++) fwrite(&precalc[i].u_noise, sizeof(FLOAT), 1, f);
+			fclose(f);
+		}
 	} else if(!strcmp(argv[1], "solve") || !strcmp(argv[1], "solvex")) {
 		const int ext = !strcmp(argv[1], "solvex");
 		const int first_T = ext ? 9 : 7;

@@ -216,7 +216,7 @@ class Simulation:
 
     def __init__(self, n1, n2, total_n3, L, calc_mode, params, nprocs=1, rank=0, beads=None,
                  initial=None, tau=1.0, tau_min=0.0, delta=1e-3, t0=0.0, gl_static=False, kz=None,
-                 init_solver=True, tile=None, recompute=True, icond=None):
+                 init_solver=True, tile=None, recompute=True, icond=None, device_ic=False):
         L1, L2, L3 = L
         self.lib = L_ = lib()
         self.grid = pft_grid()
@@ -238,7 +238,7 @@ class Simulation:
                 rc = L_.pft_ic_eval(C.byref(self.grid), q, len(prog), _ip(ops), _dp(args), _dp(self.x))
                 if rc:
                     raise ValueError(f"pft_ic_eval failed ({rc})")
-        elif initial is None:
+        elif initial is None and not device_ic:
             L_.pft_model_ic_default(_dp(self.x))
         else:
             self.set_interior(initial)
@@ -263,7 +263,8 @@ class Simulation:
         if beads is not None and initial is None:   # (also after icond formulas)
             b = np.ascontiguousarray(beads, dtype=np.float64)
             L_.pft_model_set_beads(_dp(b), b.shape[0])
-            L_.pft_model_set_solution(_dp(self.x))
+            # device_ic: the beads are overlaid on the device (pft_solver_ic_default_device)
+            L_.pft_model_set_solution(None if device_ic else _dp(self.x))
         else:
             L_.pft_model_set_solution(None)
         if L_.PrecalculateData(_dp(self.chunk_mult)):
@@ -276,6 +277,15 @@ class Simulation:
             rc = L_.RK_MPI_SA_check_mem(C.byref(self.mem))
             if rc:
                 raise RuntimeError(f"RK_MPI_SA_check_mem failed ({rc})")
+        if device_ic:
+            # f1: the default Params' IC and the beads computed on the device (bit for bit the
+            # host's); the host array receives a copy, so every later call works as after a host IC
+            assert icond is None and initial is None and self.initialised, "device_ic: default IC, solver initialised"
+            rc = L_.pft_solver_ic_default_device(1 if beads is not None else 0)
+            if rc:
+                raise RuntimeError(f"pft_solver_ic_default_device failed ({rc}): {L_.pft_hip_last_error()}")
+            if L_.pft_solver_download(C.byref(self.system)):
+                raise RuntimeError("pft_solver_download failed")
 
     # -- host array views ------------------------------------------------------------------
     def padded(self):

@@ -378,6 +378,90 @@ int pft_model_ic_default(FLOAT * w)
 	return 0;
 }
 
+/* f1: the per-axis tables of the device initial condition (pft_slab_ic_default).  Every term of
+   pft_model_ic_default and overlay_beads that depends on one coordinate only is evaluated here,
+   with the same expressions and the C library's tanh / pow; the device combines them in the same
+   order and evaluates the beads' tanh with the C library's algorithm (pft_tanh.h).  with_beads:
+   overlay the beads (PrecalculateData after the IC).  *store / *istore: the tables' memory, for
+   pft_model_ic_tables_free. */
+int pft_model_ic_tables(pft_ic_tables * t, int with_beads, double ** store, int ** istore)
+{
+	const model_state * const m = &M;
+	const double * P = M.param;
+	const double c293 = pft_float_val("293.15"), c052 = pft_float_val("0.052"),
+	             c058 = pft_float_val("0.058"), c055 = pft_float_val("0.055");
+	const int n1 = M.g.n1, n2 = M.g.n2, n3 = M.g.n3;
+	const double s = 0.5 / P[PFT_P_xi_gl];
+	double * d, bxyz[3*MAX_BALLS_COUNT];
+	int * iv, i, j, k, q, nb = 0, cnt = 0;
+	if(!M.configured) return -3;
+	if(with_beads) {
+		if(!M.beads_set) return -1;          /* the reference fails without the bead file */
+		nb = M.nbeads;
+	}
+	d = (double*)malloc(sizeof(double)*(4*(size_t)(n1 + n2 + n3) + 3*(size_t)nb));
+	iv = (int*)malloc(sizeof(int)*((size_t)(n3 + 1) + (size_t)n3*(nb > 0 ? nb : 1)));
+	if(!d || !iv) { free(d); free(iv); return -1; }
+	memset(t, 0, sizeof(*t));
+	t->n1 = n1; t->n2 = n2; t->n3 = n3;
+	t->tx1 = d; t->tx2 = d + n1; t->px2 = d + 2*n1; t->xb = d + 3*n1;
+	t->ty1 = d + 4*n1; t->ty2 = t->ty1 + n2; t->py2 = t->ty1 + 2*n2; t->yb = t->ty1 + 3*n2;
+	t->tz1 = t->ty1 + 4*n2; t->tz2 = t->tz1 + n3; t->pz = t->tz1 + 2*n3; t->zb = t->tz1 + 3*n3;
+	t->bxyz = t->tz1 + 4*n3;
+	t->u0 = c293;
+	t->r2 = pow(M.g.L1/3.0, 2.0);
+	for(i=0;i<n1;i++) {
+		const double x = m->g.L1 * ((0.5+i) / m->g.n1);                  /* pft_model_ic_default */
+		d[i] = 0.5*(1.0 + tanh(s*(x - m->g.L1 + P[PFT_P_beads_offset_x])));
+		d[n1+i] = 0.5*(1.0 + tanh(s*(P[PFT_P_beads_offset_x] - x)));
+		d[2*n1+i] = pow(x - m->g.L1/2.0, 2.0);
+		d[3*n1+i] = m->g.L1 * (0.5+i) / m->g.n1;                        /* overlay_beads */
+	}
+	for(j=0;j<n2;j++) {
+		double * e = (double*)t->ty1;
+		const double y = m->g.L2 * ((0.5+j) / m->g.n2);
+		e[j] = 0.5*(1.0 + tanh(s*(y - m->g.L2 + P[PFT_P_beads_offset_y])));
+		e[n2+j] = 0.5*(1.0 + tanh(s*(P[PFT_P_beads_offset_y] - y)));
+		e[2*n2+j] = pow(y - m->g.L2/2.0, 2.0);
+		e[3*n2+j] = m->g.L2 * (0.5+j) / m->g.n2;
+	}
+	for(k=0;k<n3;k++) {
+		double * e = (double*)t->tz1;
+		const double z = m->g.L3 * ((0.5+k+m->g.first_row) / m->g.total_n3);
+		e[k] = 0.5*(1.0 + tanh(s*(z - c055)));
+		e[n3+k] = 0.5*(1.0 + tanh(s*(P[PFT_P_beads_offset_z] - z)));
+		e[2*n3+k] = ((z > c052) && (z < c058)) ? 1.0 : 0.0;
+		e[3*n3+k] = m->g.L3 * (0.5+k+m->g.first_row) / m->g.total_n3;
+	}
+	if(nb) {
+		/* overlay_beads: the same centres, cull distance and per-plane candidate lists */
+		const double R = P[PFT_P_ball_radius];
+		const double reach = R + 2.0*P[PFT_P_xi_gl]*30.0;
+		const double reach2 = reach*reach;
+		for(q=0;q<nb;q++) {
+			bxyz[3*q+0] = M.beads[3*q+0]*P[PFT_P_beads_scaling] + P[PFT_P_beads_offset_x];
+			bxyz[3*q+1] = M.beads[3*q+1]*P[PFT_P_beads_scaling] + P[PFT_P_beads_offset_y];
+			bxyz[3*q+2] = M.beads[3*q+2]*P[PFT_P_beads_scaling] + P[PFT_P_beads_offset_z];
+		}
+		memcpy((double*)t->bxyz, bxyz, sizeof(double)*3*nb);
+		for(k=0;k<n3;k++) {
+			const double z = t->zb[k];
+			iv[k] = cnt;
+			for(q=0;q<nb;q++) { const double dz = z - bxyz[3*q+2]; if(dz*dz < reach2*1.0001) iv[n3+1+cnt++] = q; }
+		}
+		iv[n3] = cnt;
+		t->nbeads = nb;
+		t->plane_off = iv;
+		t->plane_beads = iv + n3 + 1;
+		t->s = s;
+		t->R = R;
+		t->reach2 = reach2*1.0001;
+	}
+	*store = d;
+	*istore = iv;
+	return 0;
+}
+
 /* ---------------------------------------------------------------------------------------- */
 /* right-hand sides and meta-pointers */
 

@@ -19,4 +19,8 @@ int pft_model_get_consts(pft_consts * c);
 /* host u_noise field [k][j][i] of this slab, or NULL when u_noise_amp == 0 */
 const double * pft_model_noise(void);
 
+/* f1: the per-axis tables of the device initial condition (pft_slab_ic_default) for the
+   configured slab, with or without the bead overlay; free(*store), free(*istore) afterwards */
+int pft_model_ic_tables(pft_ic_tables * t, int with_beads, double ** store, int ** istore);
+
 #endif

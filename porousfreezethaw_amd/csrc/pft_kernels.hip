@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <vector>
 #include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -28,6 +29,7 @@
 #include <string.h>
 
 #include "../../include/pft_hip.h"
+#include "pft_tanh.h"
 
 #pragma clang fp contract(off)
 
@@ -410,17 +412,21 @@ __device__ __forceinline__ void eps_arrive(double bm, int bnf, EpsShard* shards,
 // workgroups compute.  The reduction leaves the error-norm launch's critical path (its last
 // workgroups spent ~1-2 us in the arrival atomics), and the kernel boundary orders the plain stores
 // before the reads.  One block of 256 threads; called with the block's threads.
-__device__ __forceinline__ void eps_reduce_publish(const unsigned long long* __restrict__ part, int n,
-                                                   unsigned long long* pub, unsigned long long* mo = nullptr,
-                                                   unsigned long long* fo = nullptr)
+__device__ __forceinline__ void eps_part_load(const unsigned long long* __restrict__ part, int n, unsigned long long& m,
+                                              unsigned long long& f)
 {
-  __shared__ unsigned long long rm[4], rf[4];
-  unsigned long long m = 0, f = 0;
+  m = 0;
+  f = 0;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const unsigned long long b = part[2 * i], nf = part[2 * i + 1];
     m = b > m ? b : m;   // non-negative doubles (and +0) order as their bit patterns
     f |= nf;
   }
+}
+__device__ __forceinline__ void eps_part_publish(unsigned long long m, unsigned long long f, unsigned long long* pub,
+                                                 unsigned long long* mo = nullptr, unsigned long long* fo = nullptr)
+{
+  __shared__ unsigned long long rm[4], rf[4];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const unsigned long long om = __shfl_xor(m, off, 64), of = __shfl_xor(f, off, 64);
@@ -442,6 +448,14 @@ __device__ __forceinline__ void eps_reduce_publish(const unsigned long long* __r
     if (mo) *mo = m;
     if (fo) *fo = f;
   }
+}
+__device__ __forceinline__ void eps_reduce_publish(const unsigned long long* __restrict__ part, int n,
+                                                   unsigned long long* pub, unsigned long long* mo = nullptr,
+                                                   unsigned long long* fo = nullptr)
+{
+  unsigned long long m, f;
+  eps_part_load(part, n, m, f);
+  eps_part_publish(m, f, pub, mo, fo);
 }
 
 // a workgroup's contribution in the deferred form
@@ -738,21 +752,27 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
   const int WX = a.gwx, TY = a.gty, TX = 2 * WX, LW = TX + 4, LH = TY + 2, NH = LW + 2 * TY;
   __shared__ __attribute__((aligned(16))) double lds[2][3][PFT_FUSED_LF];
 
+  // A gated launch runs iff the step it belongs to was accepted, on the decided (t, h) (gate words
+  // [0] sequence, [1] t, [2] h).  The words are loaded here, beside the prologue's operand loads
+  // (which need no scalar of the step), and checked after them: one memory round trip before the
+  // stencil instead of two dependent ones (the check and then t, h) ahead of it.
+  unsigned long long gw0 = 0, gw1 = 0, gw2 = 0;
   if (a.gate) {
-    // a gated launch: run iff the step it belongs to was accepted (t, h from the decision), else
-    // leave before any store
-    const unsigned long long gs = __hip_atomic_load(a.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (gs != a.gseq) return;
-    const double gt = __longlong_as_double((long long)a.gate[1]), gh = __longlong_as_double((long long)a.gate[2]);
-    gate_scalars<STAGE>(a, c, gt, gh);
-    a.dt = gt;
-    a.dh = gh;
+    gw0 = __hip_atomic_load(a.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    gw1 = a.gate[1];
+    gw2 = a.gate[2];
   }
   if (STAGE == 1 && (a.npart > 0 || a.gdev) && (int)blockIdx.x == a.ntile * a.nchunk) {
     // the extra workgroup of a speculative stage 1: the previous launch's error norm, then (gated
     // steps) the decision on the step it ended
     unsigned long long m = 0, f = 0;
-    if (a.npart > 0) eps_reduce_publish(a.part, a.npart, a.pub, &m, &f);
+    if (a.npart > 0) eps_part_load(a.part, a.npart, m, f);
+    if (a.gate) {
+      if (gw0 != a.gseq) return;       // (uniform: every thread read the same word)
+      a.dt = __longlong_as_double((long long)gw1);
+      a.dh = __longlong_as_double((long long)gw2);
+    }
+    if (a.npart > 0) eps_part_publish(m, f, a.pub, &m, &f);
     if (a.gdev && threadIdx.x == 0) gate_decide(a, a.dt, a.dh, m, (int)f, a.npart > 0);
     return;
   }
@@ -814,16 +834,25 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
   // (re-loading them one plane later misses the 4 MiB L2: 0.52 vs 0.65 ms at 400^3)
   dbl2 cx[3], ck1[3], ck4[3], cE[3], nx[3], nk1[3], nk4[3], nE[3];
   int cur = 0;
+  const long o0 = (long)(kb + 1) * a.plane + po;
+  const bool wlo = kb == 0 && !a.has_below;
+  const long ob = wlo ? o0 : o0 - a.plane;
+  Ops cop[3], bop[3], hop;
   if (kb < ke) {
-    const long o0 = (long)(kb + 1) * a.plane + po;
-    const bool wlo = kb == 0 && !a.has_below;
-    const long ob = wlo ? o0 : o0 - a.plane;
-    Ops cop[3], bop[3], hop;
 #pragma unroll
     for (int q = 0; q < 3; ++q) load_ops<STAGE, GLS>(a, q, o0, cop[q]);
 #pragma unroll
     for (int q = 0; q < 3; ++q) load_ops<STAGE, GLS>(a, q, ob, bop[q]);
     load_ops<STAGE, GLS>(a, hf, (long)(kb + 1) * a.plane + hp, hop);
+  }
+  if (a.gate) {
+    if (gw0 != a.gseq) return;         // rejected (or NaN): leave before any store
+    const double gt = __longlong_as_double((long long)gw1), gh = __longlong_as_double((long long)gw2);
+    gate_scalars<STAGE>(a, c, gt, gh);
+    a.dt = gt;
+    a.dh = gh;
+  }
+  if (kb < ke) {
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       zc[q] = stage_in<STAGE, GLS>(a, q, cop[q]);
@@ -1028,12 +1057,19 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
 // z neighbours of both levels are read from the plane rings (own pair: written by the thread
 // itself; x/y neighbours: written one iteration earlier, behind the barrier).
 #define PFT_PBLOCK 512
-#define PFT_PAIR_PAD 4          // doubles before / after each LDS field plane: the discarded outer
-                                // cell of a ring pair reads one slot beyond its row
-#define PFT_PAIR_LP 44          // LDS row pitch (doubles): tx + 4 <= 44, a compile-time constant so
-                                // that every LDS access is a per-lane base + an immediate offset
-#define PFT_PAIR_LFA 1024       // 44 (ty + 4) + 2 pad doubles per field and plane (stage A input)
-#define PFT_PAIR_LFB 936        // 44 (ty + 2) + 2 pad (stage B input)
+// LDS layout of a field plane: the even cells of the positions (first cell of each pair) in one
+// half, the odd cells PFT_PAIR_H doubles later, position (px, py) at slot PFT_PAIR_PADP + py LWP + px
+// of each half.  A wave's lanes hold consecutive positions, so every 8-byte LDS access (a cell, or
+// a neighbour one slot or one row away) is consecutive across lanes: no bank conflicts (64 banks of
+// 4 B; interleaved pairs read at a 16-byte lane stride were 2-way conflicts, SQ_LDS_BANK_CONFLICT
+// 0.44 of the LDS cycles of pair 4+5: profiles/r04a_pmc_pair_table.txt).  PFT_PAIR_H is a multiple
+// of 32 pairs, so a mirrored lane's access to the other half falls on its own banks.
+#define PFT_PAIR_PADP 2         // slots before / after the positions of each half: the discarded
+                                // outer cell of a ring pair reads one slot beyond its row
+#define PFT_PAIR_H 512          // doubles per half (even / odd cells) of a field plane
+// The row pitch LWP (pairs) is a template parameter, a compile-time constant so that every LDS
+// access is a per-lane base + an immediate offset: 22 (tiles up to 40 cells wide, 19 rows) or 12
+// (up to 20 cells wide, 38 rows: n1 = 100 in 5 tiles of 20 where 40-wide tiles leave a sixth idle)
 #ifndef PFT_PAIR_MIN_CELLS_PER_CU
 #define PFT_PAIR_MIN_CELLS_PER_CU 16384
 #endif
@@ -1166,26 +1202,52 @@ __device__ __forceinline__ dbl2 pair_in_B(const PairArgs& a, int q, const PairRa
   return v;
 }
 
-// a pair from LDS with its halves exchanged when sw = 1 (two 8-byte reads at per-thread offsets)
-__device__ __forceinline__ dbl2 ld2x(const double* p, int sw)
+// a pair from / to the LDS halves at slot p, with its cells exchanged when sw = 1 (two 8-byte
+// accesses at per-lane offsets)
+#ifndef PFT_PAIR_SWSEL
+#define PFT_PAIR_SWSEL 1
+#endif
+__device__ __forceinline__ dbl2 ldeo(const double* L, int p, int sw)
 {
   dbl2 v;
-  v.x = p[sw];
-  v.y = p[1 - sw];
+#if PFT_PAIR_SWSEL
+  const double e = L[p], o = L[PFT_PAIR_H + p];
+  v.x = sw ? o : e;
+  v.y = sw ? e : o;
+#else
+  v.x = L[sw * PFT_PAIR_H + p];
+  v.y = L[(1 - sw) * PFT_PAIR_H + p];
+#endif
   return v;
+}
+__device__ __forceinline__ void steo(double* L, int p, dbl2 v, int sw)
+{
+#if PFT_PAIR_SWSEL
+  L[p] = sw ? v.y : v.x;
+  L[PFT_PAIR_H + p] = sw ? v.x : v.y;
+#else
+  L[sw * PFT_PAIR_H + p] = v.x;
+  L[(1 - sw) * PFT_PAIR_H + p] = v.y;
+#endif
+}
+__device__ __forceinline__ dbl2 ldeo(const double* L, int p) { return dbl2{L[p], L[PFT_PAIR_H + p]}; }
+__device__ __forceinline__ void steo(double* L, int p, dbl2 v)
+{
+  L[p] = v.x;
+  L[PFT_PAIR_H + p] = v.y;
 }
 
 // the RHS of one cell pair (du, dp of both cells): centre zc, z neighbours zm / zp, x/y
-// neighbours from the LDS field planes L[q] at slot lo (row pitch PFT_PAIR_LP); the x-face
-// between the pair's cells is evaluated once and the z-face below is carried in fz
+// neighbours from the LDS field planes L[q] around slot p (even / odd halves, row pitch LWP); the
+// x-face between the pair's cells is evaluated once and the z-face below is carried in fz
 // (rhs_cell_f, bit-exact), as in merson_fused
-template <int MODE>
+template <int MODE, int LWP>
 __device__ __forceinline__ void pair_rhs(const pft_consts& c, const double* L0, const double* L1, const double* L2,
-                                         int lo, const dbl2* zm, const dbl2* zc, const dbl2* zp,
+                                         int p, const dbl2* zm, const dbl2* zc, const dbl2* zp,
                                          const double* nz, FaceT* fz, double* du, double* dp)
 {
   constexpr bool FLUX = MODE != 10 && MODE != 11;
-  constexpr int LW = PFT_PAIR_LP;
+  constexpr int H = PFT_PAIR_H;
   const double* L[3] = {L0, L1, L2};
   FaceT fx;
 #pragma unroll
@@ -1195,10 +1257,10 @@ __device__ __forceinline__ void pair_rhs(const pft_consts& c, const double* L0, 
     for (int q = 0; q < 3; ++q) {
       const double cen = zc[q][s];
       col[q].c = cen;
-      col[q].xm = s == 0 ? L[q][lo - 1] : zc[q][0];
-      col[q].xp = s == 0 ? zc[q][1] : L[q][lo + 2];
-      col[q].ym = L[q][lo - LW + s];
-      col[q].yp = L[q][lo + LW + s];
+      col[q].xm = s == 0 ? L[q][H + p - 1] : zc[q][0];     // odd cell of the pair to the left
+      col[q].xp = s == 0 ? zc[q][1] : L[q][p + 1];         // even cell of the pair to the right
+      col[q].ym = L[q][s * H + p - LWP];
+      col[q].yp = L[q][s * H + p + LWP];
       col[q].zm = zm[q][s];
       col[q].zp = zp[q][s];
     }
@@ -1214,18 +1276,17 @@ __device__ __forceinline__ void pair_rhs(const pft_consts& c, const double* L0, 
 template <int N>
 using pft_ic = std::integral_constant<int, N>;
 
-template <int SA, int MODE, bool GLX>
+template <int SA, int MODE, bool GLX, int LWP>
 __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2))) void merson_pair(PairArgs a,
                                                                                                    pft_consts c)
 {
   constexpr bool FLUX = MODE != 10 && MODE != 11;
   constexpr dbl2 zero2 = {0.0, 0.0};
-  constexpr int LW = PFT_PAIR_LP;
 #if defined(__HIP_DEVICE_COMPILE__)
   const pft_kptr kbase = (pft_kptr)__builtin_amdgcn_kernarg_segment_ptr();
 #endif
-  __shared__ __attribute__((aligned(16))) double lA[3][3][PFT_PAIR_LFA];
-  __shared__ __attribute__((aligned(16))) double lB[3][3][PFT_PAIR_LFB];
+  __shared__ __attribute__((aligned(16))) double lA[3][3][2 * PFT_PAIR_H];
+  __shared__ __attribute__((aligned(16))) double lB[3][3][2 * PFT_PAIR_H];
 
   const int TX = a.tx, TY = a.ty, WP2 = TX / 2 + 2, NPOS = WP2 * (TY + 4);
   const int lin = xcd_remap(blockIdx.x, a.ntile * a.nchunk);
@@ -1242,9 +1303,9 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   const unsigned apo = (unsigned)(aj * a.n1 + ai);
   // byte offset of the acting pair in plane m of a field, from the PairArgs pointers
   auto pbo = [&](int m) -> unsigned { return ((unsigned)(m + 2) * (unsigned)a.plane + apo) * 8u; };
-  const int posA = PFT_PAIR_PAD + py * LW + 2 * px;            // this position in lA
-  const int posB = PFT_PAIR_PAD + (py - 1) * LW + 2 * px;      // ... in lB (rows 1..ty+2)
-  const int actA = PFT_PAIR_PAD + (aj - y0 + 2) * LW + (ai - x0 + 2);   // the acting pair in lA
+  const int posA = PFT_PAIR_PADP + py * LWP + px;              // this position's slot in lA
+  const int posB = PFT_PAIR_PADP + (py - 1) * LWP + px;        // ... in lB (rows 1..ty+2)
+  const int actA = PFT_PAIR_PADP + (aj - y0 + 2) * LWP + (ai - x0 + 2) / 2;   // the acting pair in lA
   const bool isA = py >= 1 && py <= TY + 2;
   const bool isB = (int)threadIdx.x < NPOS && px >= 1 && px <= TX / 2 && py >= 2 && py <= TY + 1 &&
                    pi < a.n1 && pj < a.n2;
@@ -1284,18 +1345,18 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         iam[q] = pair_in_A<SA, GLX>(a, q, t);
-        st2x(&lA[2][q][posA], iam[q], xsw);
+        steo(lA[2][q], posA, iam[q], xsw);
       }
     }
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       ia0[q] = pair_in_A<SA, GLX>(a, q, R[0]);
-      st2x(&lA[0][q][posA], ia0[q], xsw);
+      steo(lA[0][q], posA, ia0[q], xsw);
       if (mA0 == mfirst) {
         // bottom wall: plane -1 mirrors plane 0 (equation.c:164-174), also in the ring slot of
         // plane -1, so that the z-loop reads its z neighbours without selects
         iam[q] = ia0[q];
-        st2x(&lA[2][q][posA], ia0[q], xsw);
+        steo(lA[2][q], posA, ia0[q], xsw);
       }
     }
 #pragma unroll
@@ -1320,7 +1381,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
       // placement lost track of them and stage A waited for the look-ahead it had just issued.
       if (mm + 1 <= mlast) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) st2x(&lA[sAp][q][posA], pair_in_A<SA, GLX>(A0, q, rn), xsw);
+        for (int q = 0; q < 3; ++q) steo(lA[sAp][q], posA, pair_in_A<SA, GLX>(A0, q, rn), xsw);
       }
       if (mm + 2 <= mlast) pair_load<SA>(A0, pbo(mm + 2), rnn);          // look-ahead
     }
@@ -1342,29 +1403,26 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
           // top wall: the ring slot of plane n3 holds the ghost values -- Dirichlet u (equation.c:
           // 175-183), p and gl mirrored -- at this position (its own z neighbour only)
 #pragma unroll
-          for (int q = 1; q < 3; ++q) {
-            lA[sAp][q][posA] = lA[sA][q][posA];
-            lA[sAp][q][posA + 1] = lA[sA][q][posA + 1];
-          }
-          lA[sAp][0][posA] = lA[sAp][0][posA + 1] = A1.T_topA;
+          for (int q = 1; q < 3; ++q) steo(lA[sAp][q], posA, ldeo(lA[sA][q], posA));
+          steo(lA[sAp][0], posA, dbl2{A1.T_topA, A1.T_topA});
         }
         dbl2 zc[3], zm[3], zp[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          zc[q] = ld2x(&lA[sA][q][posA], xsw);
-          zm[q] = ld2x(&lA[sAm][q][posA], xsw);
-          zp[q] = ld2x(&lA[sAp][q][posA], xsw);
+          zc[q] = ldeo(lA[sA][q], posA, xsw);
+          zm[q] = ldeo(lA[sAm][q], posA, xsw);
+          zp[q] = ldeo(lA[sAp][q], posA, xsw);
         }
         double du[2], dp[2];
         const double* nz = A1.noise ? A1.noise + (long)mm * A1.plane + (long)apo : nullptr;
-        pair_rhs<MODE>(C1, &lA[sA][0][0], &lA[sA][1][0], &lA[sA][2][0], actA, zm, zc, zp, nz, fzA, du, dp);
+        pair_rhs<MODE, LWP>(C1, lA[sA][0], lA[sA][1], lA[sA][2], actA, zm, zc, zp, nz, fzA, du, dp);
         ka[0] = dbl2{du[0], du[1]};
         ka[1] = dbl2{dp[0], dp[1]};
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
           const dbl2 ib = pair_in_B<SA, GLX>(A1, q, rc, q < 2 ? ka[q < 2 ? q : 0] : zero2);
-          st2x(&lB[sA][q][posB], ib, xsw);
-          if (mm == 0 && wlo) st2x(&lB[sAm][q][posB], ib, xsw);   // bottom wall: plane -1 mirrors plane 0
+          steo(lB[sA][q], posB, ib, xsw);
+          if (mm == 0 && wlo) steo(lB[sAm][q], posB, ib, xsw);   // bottom wall: plane -1 mirrors plane 0
         }
       }
     }
@@ -1389,15 +1447,15 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
         if (kB == n3 - 1 && whi) {
           // top wall: the ghost values of plane n3 at this position (as in stage A above)
 #pragma unroll
-          for (int q = 1; q < 3; ++q) st2(&lB[sBp][q][lo], ld2(&lB[sB][q][lo]));
-          st2(&lB[sBp][0][lo], dbl2{A2.T_topB, A2.T_topB});
+          for (int q = 1; q < 3; ++q) steo(lB[sBp][q], lo, ldeo(lB[sB][q], lo));
+          steo(lB[sBp][0], lo, dbl2{A2.T_topB, A2.T_topB});
         }
         dbl2 zc[3], zm[3], zp[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          zc[q] = ld2(&lB[sB][q][lo]);
-          zm[q] = ld2(&lB[sBm][q][lo]);
-          zp[q] = ld2(&lB[sBp][q][lo]);
+          zc[q] = ldeo(lB[sB][q], lo);
+          zm[q] = ldeo(lB[sBm][q], lo);
+          zp[q] = ldeo(lB[sBp][q], lo);
         }
         if (kB == kb) {
           // the z-face below the chunk's first stage-B plane
@@ -1408,7 +1466,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
         double du[2], dp[2];
         const unsigned e0 = pbo(kB);
         const double* nz = A2.noise ? A2.noise + (long)kB * A2.plane + (long)apo : nullptr;
-        pair_rhs<MODE>(C2, &lB[sB][0][0], &lB[sB][1][0], &lB[sB][2][0], lo, zm, zc, zp, nz, fzB, du, dp);
+        pair_rhs<MODE, LWP>(C2, lB[sB][0], lB[sB][1], lB[sB][2], lo, zm, zc, zp, nz, fzB, du, dp);
         if (SA == 2) {
           stb(A2.out, e0, dbl2{du[0], du[1]});                   // K3 (hybrid2.c:412-429)
           stb(A2.out + A2.fs, e0, dbl2{dp[0], dp[1]});
@@ -1476,6 +1534,67 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
       else eps_arrive(bm, bnf, a.shards, a.eps_bits, a.nonfinite, a.pub, a.pub_count);
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// f1: the default Params' initial condition and the glass beads on the device (pft_slab_ic_default)
+
+struct IcDev {
+  double* x;             // X
+  double* xn;            // XN (the same values)
+  long fs;
+  int n1, n2, n3, plane;
+  const double* tab;     // tx1 tx2 px2 xb [n1], ty1 ty2 py2 yb [n2], tz1 tz2 pz zb [n3], beads 3*nb
+  const int* poff;       // [n3 + 1]
+  const int* pbead;
+  int nbeads;
+  double u0, r2, s, R, reach2;
+  unsigned int* unclean;
+};
+
+// one thread per interior node: pft_model_ic_default (Params:9-21 as the reference's evaluator
+// computes them: u = 293.15; p = 1 inside the ice disc, else 0; gl the max of the six wall terms in
+// the formula's order) and overlay_beads (equation.c:507-530: gl = max(gl, 0.5 (1 - tanh(s (|x -
+// b| + 1e-10 - R))))), every operation the host's in the host's order, no contraction
+__global__ __launch_bounds__(256) void ic_default_kernel(IcDev a)
+{
+  const long n = (long)a.plane * a.n3;
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const int k = (int)(e / a.plane);
+  const int r = (int)(e - (long)k * a.plane);
+  const int j = r / a.n1, i = r - j * a.n1;
+  const double* X = a.tab;
+  const double* Y = X + 4 * a.n1;
+  const double* Z = Y + 4 * a.n2;
+  const double* B = Z + 4 * a.n3;
+  const double p = (Z[2 * a.n3 + k] != 0.0 && X[2 * a.n1 + i] + Y[2 * a.n2 + j] < a.r2) ? 1.0 : 0.0;
+  double gl = Z[k];
+  gl = gl > Z[a.n3 + k] ? gl : Z[a.n3 + k];           // evmax (ee_wrapper.cc:246-250), in order
+  gl = gl > X[i] ? gl : X[i];
+  gl = gl > Y[j] ? gl : Y[j];
+  gl = gl > X[a.n1 + i] ? gl : X[a.n1 + i];
+  gl = gl > Y[a.n2 + j] ? gl : Y[a.n2 + j];
+  if (a.nbeads) {
+    const double x = X[3 * a.n1 + i], y = Y[3 * a.n2 + j], z = Z[3 * a.n3 + k];
+    for (int t = a.poff[k]; t < a.poff[k + 1]; ++t) {
+      const int b = a.pbead[t];
+      const double v1 = x - B[3 * b], v2 = y - B[3 * b + 1], v3 = z - B[3 * b + 2];
+      const double d2 = v1 * v1 + v2 * v2 + v3 * v3;
+      if (d2 > a.reach2) continue;
+      const double nrm = sqrt(d2) + 1E-10;
+      const double phf = 0.5 * (1.0 - pft_tanh(a.s * (nrm - a.R)));
+      if (gl < phf) gl = phf;
+    }
+  }
+  const long o = (long)(k + 1) * a.plane + r;
+  a.x[o] = a.u0;
+  a.x[a.fs + o] = p;
+  a.x[2 * a.fs + o] = gl;
+  a.xn[o] = a.u0;
+  a.xn[a.fs + o] = p;
+  a.xn[2 * a.fs + o] = gl;
+  if (gl != gl || (gl == 0.0 && signbit(gl))) atomicOr(a.unclean, 1u);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2508,6 +2627,73 @@ int pft_slab_set_noise(pft_slab* s, const double* host_noise)
   return 0;
 }
 
+int pft_slab_ic_default(pft_slab* s, const pft_ic_tables* t, int* gl_unclean)
+{
+  if (!t || t->n1 != s->d.n1 || t->n2 != s->d.n2 || t->n3 != s->d.n3) return -2;
+  const int n1 = t->n1, n2 = t->n2, n3 = t->n3, nb = t->nbeads;
+  const long nbi = nb ? t->plane_off[n3] : 0;
+  const size_t nd = 4 * (size_t)(n1 + n2 + n3) + 3 * (size_t)nb;
+  const size_t ni = (size_t)(n3 + 1) + (size_t)nbi;
+  std::vector<double> hd(nd);
+  std::vector<int> hi(ni, 0);
+  const double* src[12] = {t->tx1, t->tx2, t->px2, t->xb, t->ty1, t->ty2, t->py2, t->yb,
+                           t->tz1, t->tz2, t->pz, t->zb};
+  const int len[3] = {n1, n2, n3};
+  size_t o = 0;
+  for (int a = 0; a < 3; ++a)
+    for (int q = 0; q < 4; ++q) {
+      memcpy(&hd[o], src[4 * a + q], sizeof(double) * len[a]);
+      o += len[a];
+    }
+  if (nb) {
+    memcpy(&hd[o], t->bxyz, sizeof(double) * 3 * nb);
+    memcpy(&hi[0], t->plane_off, sizeof(int) * (n3 + 1));
+    if (nbi) memcpy(&hi[n3 + 1], t->plane_beads, sizeof(int) * nbi);
+  }
+  double* dd = nullptr;
+  int* di = nullptr;
+  unsigned int* du = nullptr;
+  IcDev a;
+  memset(&a, 0, sizeof(a));
+  hipError_t e = hipMalloc((void**)&dd, sizeof(double) * nd);
+  if (e == hipSuccess) e = hipMalloc((void**)&di, sizeof(int) * ni);
+  if (e == hipSuccess) e = hipMalloc((void**)&du, sizeof(unsigned int));
+  if (e == hipSuccess) e = hipMemcpyAsync(dd, hd.data(), sizeof(double) * nd, hipMemcpyHostToDevice, s->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(di, hi.data(), sizeof(int) * ni, hipMemcpyHostToDevice, s->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(du, 0, sizeof(unsigned int), s->stream);
+  if (e == hipSuccess) {
+    a.x = s->buf[PFT_BUF_X];
+    a.xn = s->buf[PFT_BUF_XN];
+    a.fs = s->fs;
+    a.n1 = n1;
+    a.n2 = n2;
+    a.n3 = n3;
+    a.plane = s->plane;
+    a.tab = dd;
+    a.poff = di;
+    a.pbead = di + n3 + 1;
+    a.nbeads = nb;
+    a.u0 = t->u0;
+    a.r2 = t->r2;
+    a.s = t->s;
+    a.R = t->R;
+    a.reach2 = t->reach2;
+    a.unclean = du;
+    const long n = (long)s->plane * n3;
+    ic_default_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s->stream>>>(a);
+    e = hipGetLastError();
+  }
+  unsigned int hu = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(&hu, du, sizeof(unsigned int), hipMemcpyDeviceToHost, s->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+  (void)hipFree(dd);
+  (void)hipFree(di);
+  (void)hipFree(du);
+  if (e != hipSuccess) return fail(e, "pft_slab_ic_default");
+  if (gl_unclean) *gl_unclean = hu ? 1 : 0;
+  return 0;
+}
+
 int pft_slab_order(pft_slab* s, int comm_first)
 {
   // the second stream waits for the work enqueued so far on the first
@@ -2769,16 +2955,23 @@ int pft_slab_stage_spec(pft_slab* s, double t_stage, int k_begin, int k_end)
 
 // ---- pair kernels (merson_pair): stages 2+3 and 4+5 of a step, one launch each -------------
 
-template <int SA, bool GLX>
-static void launch_pair_mode(int mode, dim3 g, hipStream_t st, const PairArgs& a, const pft_consts& c)
+template <int SA, bool GLX, int LWP>
+static void launch_pair_lwp(int mode, dim3 g, hipStream_t st, const PairArgs& a, const pft_consts& c)
 {
   switch (mode) {
-    case 0: merson_pair<SA, 0, GLX><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
-    case 1: merson_pair<SA, 1, GLX><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
-    case 2: merson_pair<SA, 2, GLX><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
-    case 10: merson_pair<SA, 10, GLX><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
-    case 11: merson_pair<SA, 11, GLX><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
+    case 0: merson_pair<SA, 0, GLX, LWP><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
+    case 1: merson_pair<SA, 1, GLX, LWP><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
+    case 2: merson_pair<SA, 2, GLX, LWP><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
+    case 10: merson_pair<SA, 10, GLX, LWP><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
+    case 11: merson_pair<SA, 11, GLX, LWP><<<g, PFT_PBLOCK, 0, st>>>(a, c); break;
   }
+}
+
+template <int SA, bool GLX>
+static void launch_pair_mode(int mode, int lwp, dim3 g, hipStream_t st, const PairArgs& a, const pft_consts& c)
+{
+  if (lwp == 12) launch_pair_lwp<SA, GLX, 12>(mode, g, st, a, c);
+  else launch_pair_lwp<SA, GLX, 22>(mode, g, st, a, c);
 }
 
 template <int SA, bool GLX>
@@ -2787,46 +2980,51 @@ static int pair_occupancy_mode(int mode)
   static int cache[12] = {0};
   int& n = cache[mode];
   if (n) return n;
-  const void* f = mode == 0 ? (const void*)merson_pair<SA, 0, GLX>
-                : mode == 1 ? (const void*)merson_pair<SA, 1, GLX>
-                : mode == 2 ? (const void*)merson_pair<SA, 2, GLX>
-                : mode == 10 ? (const void*)merson_pair<SA, 10, GLX>
-                             : (const void*)merson_pair<SA, 11, GLX>;
+  const void* f = mode == 0 ? (const void*)merson_pair<SA, 0, GLX, 22>
+                : mode == 1 ? (const void*)merson_pair<SA, 1, GLX, 22>
+                : mode == 2 ? (const void*)merson_pair<SA, 2, GLX, 22>
+                : mode == 10 ? (const void*)merson_pair<SA, 10, GLX, 22>
+                             : (const void*)merson_pair<SA, 11, GLX, 22>;
   int b = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, PFT_PBLOCK, 0) != hipSuccess || b < 1) b = 1;
   n = b;
   return n;
 }
 
+// the LDS row pitch (pairs) of a pair tile tx cells wide: 12 up to 20 cells, 22 up to 40
+static int pair_lwp(int tx) { return tx <= 20 ? 12 : 22; }
+
 // pair tile: tx cells (even) x ty rows; its R2 positions ((tx/2 + 2) pairs x (ty + 4) rows) one
-// per thread, and the two LDS plane rings within their static sizes
+// per thread, and the two LDS plane rings (rows of pair_lwp(tx) slots) within their halves
 static bool pair_geometry_ok(int tx, int ty)
 {
-  return tx >= 2 && tx % 2 == 0 && ty >= 1 && (tx / 2 + 2) * (ty + 4) <= PFT_PBLOCK &&
-         tx + 4 <= PFT_PAIR_LP && PFT_PAIR_LP * (ty + 4) + 2 * PFT_PAIR_PAD <= PFT_PAIR_LFA &&
-         PFT_PAIR_LP * (ty + 2) + 2 * PFT_PAIR_PAD <= PFT_PAIR_LFB;
+  const int lwp = pair_lwp(tx);
+  return tx >= 2 && tx % 2 == 0 && ty >= 1 && (tx / 2 + 2) * (ty + 4) <= PFT_PBLOCK && tx / 2 + 2 <= 22 &&
+         2 * PFT_PAIR_PADP + lwp * (ty + 4) <= PFT_PAIR_H;
 }
 
 // automatic tile: the fewest workgroups per plane (a workgroup-plane costs about the same whatever
 // the tile's edge tiles hold), of those the one with the fewest idle tile cells, then the wider.
 // n1 = 200 / 400: 40 x 19 cells (5 x 11 / 10 x 22 tiles, 462 of 512 threads evaluate stage A and
-// 380 stage B).  Returns the tiles per plane, 0 when no tile fits (n1 odd).
+// 380 stage B); n1 = 100: 20 x 34 cells (5 x 3 tiles, 98% of their cells in the plane, against 18
+// 34 x 19 tiles with the 22-pair pitch alone).  Returns the tiles per plane, 0 when no tile fits
+// (n1 odd).
 static long pair_geometry(int n1, int n2, int* tx_out, int* ty_out)
 {
   long best = 0, best_idle = 0;
   int bx = 0, by = 0;
   if (n1 < 2 || n1 % 2 || n2 < 1) return 0;
-  for (int tx = 2; tx <= n1 + 1 && tx <= 2 * PFT_PBLOCK; tx += 2) {
-    int ty = std::min(n2, PFT_PBLOCK);
-    while (ty >= 1 && !pair_geometry_ok(tx, ty)) --ty;
-    if (ty < 1) continue;
-    const long nt = (long)((n1 + tx - 1) / tx) * ((n2 + ty - 1) / ty);
-    const long idle = nt * tx * ty - (long)n1 * n2;
-    if (best == 0 || nt < best || (nt == best && idle <= best_idle)) {
-      best = nt;
-      best_idle = idle;
-      bx = tx;
-      by = ty;
+  for (int tx = 2; tx <= n1 + 1 && tx <= 40; tx += 2) {
+    for (int ty = std::min(n2, PFT_PBLOCK); ty >= 1; --ty) {
+      if (!pair_geometry_ok(tx, ty)) continue;
+      const long nt = (long)((n1 + tx - 1) / tx) * ((n2 + ty - 1) / ty);
+      const long idle = nt * tx * ty - (long)n1 * n2;
+      if (best == 0 || nt < best || (nt == best && idle <= best_idle)) {
+        best = nt;
+        best_idle = idle;
+        bx = tx;
+        by = ty;
+      }
     }
   }
   *tx_out = bx;
@@ -2930,12 +3128,13 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
   }
   const dim3 g((unsigned)(a.ntile * a.nchunk));
   const hipStream_t st = s->stream;
+  const int lwp = pair_lwp(a.tx);
   if (first == 2) {
-    if (glx) launch_pair_mode<2, true>(mode, g, st, a, s->c);
-    else launch_pair_mode<2, false>(mode, g, st, a, s->c);
+    if (glx) launch_pair_mode<2, true>(mode, lwp, g, st, a, s->c);
+    else launch_pair_mode<2, false>(mode, lwp, g, st, a, s->c);
   } else {
-    if (glx) launch_pair_mode<4, true>(mode, g, st, a, s->c);
-    else launch_pair_mode<4, false>(mode, g, st, a, s->c);
+    if (glx) launch_pair_mode<4, true>(mode, lwp, g, st, a, s->c);
+    else launch_pair_mode<4, false>(mode, lwp, g, st, a, s->c);
   }
   HIPCHK(hipGetLastError());
   return 0;

@@ -685,6 +685,35 @@ int pft_solver_download(RK_MPI_S_SOLUTION * system)
 	return pft_slab_download_host(R.slab, PFT_BUF_X, system->x);
 }
 
+int pft_solver_ic_default_device(int with_beads)
+{
+	/* f1: the default Params' IC (and the glass beads) computed on the device into X and XN, bit
+	   for bit what pft_model_ic_default + PrecalculateData give on the host; the next
+	   pft_solve_ex(..., PFT_SOLVE_REUSE_DEVICE) starts from it.  Collective with nprocs > 1 (the
+	   ghost planes are exchanged, as at an upload, and the ranks agree on gl_keep). */
+	pft_comm * c = comm();
+	pft_ic_tables tb;
+	double * store = NULL;
+	int * istore = NULL, unclean = 0, rc;
+	long long u;
+	if(R.max_n == 0) return -3;
+	if((rc = ensure_slab())) { R.last_status = rc; return PFT_SOLVE_DEVICE_ERROR; }
+	if((rc = pft_model_ic_tables(&tb, with_beads, &store, &istore))) return rc;
+	rc = pft_slab_ic_default(R.slab, &tb, &unclean);
+	free(store);
+	free(istore);
+	if(rc) { R.last_status = rc; return PFT_SOLVE_DEVICE_ERROR; }
+	u = unclean;
+	if(pft_comm_size(c) > 1) {
+		if((rc = pft_comm_allreduce_max_i64(c, &u)) || (rc = pft_comm_halo(c, PFT_BUF_X, 0, 3)) ||
+		   (rc = pft_comm_halo(c, PFT_BUF_XN, 0, 3))) { R.last_status = rc; return PFT_SOLVE_DEVICE_ERROR; }
+	}
+	pft_slab_set_gl_keep(R.slab, !u);
+	R.device_valid = 1;
+	R.k1_keep = 0;
+	return 0;
+}
+
 int pft_solver_eval_rhs(FLOAT t, const FLOAT * w, FLOAT * dw)
 {
 	/* f(t, w, dw) on host arrays: stage w into A0, exchange its boundary planes, K into K1 */

@@ -51,6 +51,8 @@ def lib():
                                    C.c_long, EXCHANGE_FN, ALLREDUCE_FN, C.c_void_p]
         L.pft_or_solve.restype = C.c_int
         L.pft_or_ic_default.argtypes = [C.POINTER(Grid), dp, dp, C.c_int, dp]
+        L.pft_or_set_noise.argtypes = [dp]
+        L.pft_or_set_noise.restype = None
         L.pft_or_float_val.argtypes = [C.c_char_p]
         L.pft_or_float_val.restype = C.c_double
         L.pft_or_decompose.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int)]
@@ -103,8 +105,10 @@ def unpad(g, w):
     return np.ascontiguousarray(w[:, BT:BT + g.n3, BT:BT + g.n2, BT:BT + g.n1])
 
 
-def rhs(info, P, mode, t, state, nprocs=1):
-    """K = f(t, state) on `nprocs` slabs held in this process (local exchange)"""
+def rhs(info, P, mode, t, state, nprocs=1, noise=None):
+    """K = f(t, state) on `nprocs` slabs held in this process (local exchange); noise: the single
+    slab's u_noise field [k][j][i] (equation.c:450-456) or None"""
+    assert noise is None or nprocs == 1
     grids = [make_grid(info, nprocs, r) for r in range(nprocs)]
     ws = [pad(g, state) for g in grids]
     dws = [np.zeros_like(w) for w in ws]
@@ -116,24 +120,40 @@ def rhs(info, P, mode, t, state, nprocs=1):
         wp = (C.POINTER(C.c_double) * nprocs)(*[ptr(w) for w in ws])
         L.pft_or_exchange_local(arr, wp, nprocs)
     for g, w, dw in zip(grids, ws, dws):
-        L.pft_or_stencil(C.byref(g), ptr(P), mode, ptr(w), None, ptr(dw))
+        L.pft_or_stencil(C.byref(g), ptr(P), mode, ptr(w),
+                         None if noise is None else ptr(np.ascontiguousarray(noise, dtype=np.float64)), ptr(dw))
     out = np.concatenate([unpad(g, dw) for g, dw in zip(grids, dws)], axis=1)
     return out, ws
 
 
-def solve(info, P, mode, state, t0, h0, times, max_steps_total=0):
-    """single-slab Merson solve to each time in `times`; returns [(t,h,steps,total,rc,state)]"""
+def solve(info, P, mode, state, t0, h0, times, max_steps_total=0, noise=None):
+    """single-slab Merson solve to each time in `times`; returns [(t,h,steps,total,rc,state)];
+    noise: the u_noise field [k][j][i] its right-hand side adds (equation.c:676-687) or None"""
     g = make_grid(info)
     x = pad(g, state)
     t, h = C.c_double(t0), C.c_double(h0)
     steps, total = C.c_long(0), C.c_long(0)
     res = []
-    for T in times:
-        rc = lib().pft_or_solve(C.byref(g), ptr(P), mode, T, C.byref(t), C.byref(h), info["tau_min"],
-                                info["delta"], 0, ptr(x), C.byref(steps), C.byref(total),
-                                max_steps_total, EXCHANGE_FN(), ALLREDUCE_FN(), None)
-        res.append((t.value, h.value, steps.value, total.value, rc, unpad(g, x)))
+    nz = None if noise is None else np.ascontiguousarray(noise, dtype=np.float64)
+    lib().pft_or_set_noise(None if nz is None else ptr(nz))
+    try:
+        for T in times:
+            rc = lib().pft_or_solve(C.byref(g), ptr(P), mode, T, C.byref(t), C.byref(h), info["tau_min"],
+                                    info["delta"], 0, ptr(x), C.byref(steps), C.byref(total),
+                                    max_steps_total, EXCHANGE_FN(), ALLREDUCE_FN(), None)
+            res.append((t.value, h.value, steps.value, total.value, rc, unpad(g, x)))
+    finally:
+        lib().pft_or_set_noise(None)
     return res
+
+
+def glibc_noise(amp, n, seed=1):
+    """u_noise = amp (rand()/RAND_MAX - 0.5) for n nodes (equation.c:450-456) from glibc's rand()
+    after srand(seed) -- what the reference draws when nothing seeded rand() (seed 1)"""
+    libc = C.CDLL("libc.so.6")
+    libc.srand(seed)
+    r = np.array([libc.rand() for _ in range(n)], dtype=np.float64)
+    return amp * (r / 2147483647.0 - 0.5)
 
 
 def ic_default(info, P, beads, nprocs=1, rank=0):

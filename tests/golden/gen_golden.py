@@ -27,6 +27,11 @@ Cases (SURVEY.md section 4.2 KATs 1-4):
   g200     BASELINE configs[1]: grid_nodes 200 (100x100x200), the same record for calc_mode 0 to
            t = 0.01 and 0.03 s (35 and 65 attempted steps) and calc_mode 1 to t = 0.03 s; run on
            8 MPI ranks and checked identical on 3.
+  gnoise   the g20 grid with u_noise_amp = 0.5 K (every published Params has 0): the noise field
+           the reference draws (glibc rand() from seed 1, equation.c:450-456), the RHS of the four
+           models that add it (calc_mode 0/10 GradP, 1/11 SigmaP1-P, equation.c:676-687) at t = 0,
+           and the mode-0 and mode-1 trajectories to t = 36 and 360 s.  One MPI rank: rand() runs
+           per rank, so the field depends on the decomposition.
   g400     BASELINE configs[2]: grid_nodes 400 (200x200x400, 16 M cells), calc_mode 0 to
            t = 0.002 and 0.005 s (about 45 and 67 attempted steps); run on 8 MPI ranks and checked
            identical on 5 (about 3 minutes of the build container's 8 cores).
@@ -202,6 +207,55 @@ def case_g20nf():
             meta[f"m{mode}_params"] = hexify(p)
         finally:
             wm.close()
+    return arrays, meta
+
+
+NOISE_AMP = 0.5
+
+
+def case_gnoise():
+    arrays, meta = {}, {"case": "gnoise", "source": f"reference Params, grid_nodes 20, u_noise_amp {NOISE_AMP}",
+                        "u_noise_amp": NOISE_AMP}
+    times = [36.0, 360.0]
+    meta["traj_times"] = times
+    noise = None
+    for mode in (0, 1, 10, 11):
+        w = Work({"grid_nodes": 20, "calc_mode": mode, "u_noise_amp": NOISE_AMP})
+        try:
+            o = w.run(1, "setup")
+            p = read_params(o)
+            shape = (3, p["n3"], p["n2"], p["n1"])
+            ic = load(os.path.join(o, "ic.f64"), shape)
+            icp = os.path.join(w.dir, "ic.f64")
+            ic.tofile(icp)
+            if mode == 0:
+                meta["params"] = hexify(p)
+                arrays["ic"] = ic
+            else:
+                assert np.array_equal(ic, arrays["ic"])
+            meta[f"m{mode}_params"] = hexify(p)
+            if mode in (0, 1):
+                o1 = w.run(1, "solve", icp, 0.0, 1.0, *times)
+                tm, st = traj(o1, len(times), shape)
+                for i, x in enumerate(st):
+                    arrays[f"traj_m{mode}_state{i}"] = x
+                meta[f"traj_m{mode}"] = tm
+            # the RHS at the mode-0 state of t = 360 s, where p is mixed (the IC's pure 0 / 1 phases
+            # switch the SigmaP1-P source term, and with it the noise, off)
+            sp = os.path.join(w.dir, "s.f64")
+            arrays["traj_m0_state1"].tofile(sp)
+            o = w.run(1, "rhs", sp, times[1])
+            arrays[f"rhs_m{mode}"] = load(os.path.join(o, "rhs.f64"), shape)
+            nz = np.fromfile(os.path.join(o, "noise_rank0.f64"), dtype="<f8").reshape(shape[1:])
+            if noise is None:
+                noise = nz
+                arrays["noise"] = nz
+            else:
+                assert np.array_equal(nz, noise)
+        finally:
+            w.close()
+    meta["rhs_state"] = "traj_m0_state1"
+    meta["rhs_time"] = times[1]
     return arrays, meta
 
 
@@ -398,7 +452,7 @@ def main():
     if not os.path.exists(PFT_REF):
         sys.exit("build the reference harness first: make -C oracle ref")
     cases = {"g20": case_g20, "ragged": case_ragged, "g100": case_g100, "ctl": case_ctl, "g200": case_g200,
-             "g400": case_g400, "g20nf": case_g20nf}
+             "g400": case_g400, "g20nf": case_g20nf, "gnoise": case_gnoise}
     for name in sys.argv[1:] or list(cases):
         arrays, meta = cases[name]()
         name = meta["case"]

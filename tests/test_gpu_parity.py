@@ -462,3 +462,52 @@ def test_gl_negative_zero_keeps_reference_bits(flavour):
     assert np.array_equal(got, res[5])
     assert np.array_equal(np.signbit(got[2]), np.signbit(res[5][2]))
     sim.close()
+
+
+# ---- u_noise pinned to the reference (tests/golden/gnoise, u_noise_amp = 0.5 K, one rank) ------
+
+def _noise_sim(meta, A, mode, initial, **kw):
+    """libpft's model set up as the reference's: its PrecalculateData draws the noise field from
+    the C library's rand() (equation.c:450-456), seeded here as the reference harness leaves it"""
+    C.CDLL("libc.so.6").srand(1)
+    sim, Pm, info = make_sim({"params": meta[f"m{mode}_params"]}, initial, mode=mode, **kw)
+    n = info["n1"] * info["n2"] * info["n3"]
+    noise = np.ctypeslib.as_array(P.lib().pft_model_noise(), shape=(n,)).copy()
+    assert np.array_equal(noise.reshape(A["noise"].shape), A["noise"]), "libpft's noise field differs"
+    return sim
+
+
+@pytest.mark.parametrize("mode", [0, 10, 1, 11])
+@pytest.mark.parametrize("flavour", ["default", "fused32", "fusedauto", "cache"])
+def test_noise_rhs_equals_reference(mode, flavour):
+    """libpft's noise field and the device RHS of the four models that add it (equation.c:676,
+    687) equal the reference's, at a state with mixed phases"""
+    meta, A = O.load_case("gnoise")
+    sim = _noise_sim(meta, A, mode, A[meta["rhs_state"]], init_solver=False, flavour=flavour)
+    dw, _ = P.rhs(sim, meta["rhs_time"])
+    K = dw.reshape((3,) + sim.N)[:, 2:-2, 2:-2, 2:-2]
+    sim.close()
+    assert np.array_equal(K, A[f"rhs_m{mode}"])
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("flavour", ["default", "fusedauto", "cache", "pairs"])
+def test_noise_trajectory_equals_reference(mode, flavour):
+    """RK_MPI_SA_solve with u_noise to t = 36 and 360 s: t, h, step counts and fields equal the
+    reference's (the pair kernels forced: both stages of a pair see the noise)"""
+    meta, A = O.load_case("gnoise")
+    pair = flavour == "pairs"
+    P.lib().pft_solver_set_option(P.PFT_OPT_PAIR, 2 if pair else 0)
+    try:
+        sim = _noise_sim(meta, A, mode, A["ic"], flavour="fusedauto" if pair else flavour)
+        for i, T in enumerate(meta["traj_times"]):
+            rc = sim.solve(T)
+            ref = meta[f"traj_m{mode}"][i]
+            assert (sim.t.hex(), sim.h.hex(), sim.system.steps, sim.system.steps_total, rc) == \
+                (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(), ref[2], ref[3], ref[4])
+            assert np.array_equal(sim.interior(), A[f"traj_m{mode}_state{i}"])
+        st = sim.stats()
+        sim.close()
+    finally:
+        P.lib().pft_solver_set_option(P.PFT_OPT_PAIR, 1)
+    assert st.path == 1 and st.pairs == (1 if pair else 0)

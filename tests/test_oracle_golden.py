@@ -111,3 +111,41 @@ def test_trajectory_no_flux_modes_bitwise(mode):
         assert (t.hex(), h.hex(), s, st, rc) == (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(),
                                                  ref[2], ref[3], ref[4])
         assert np.array_equal(x, A[f"traj_m{mode}_state{i}"])
+
+
+# ---- u_noise (tests/golden/gnoise: the reference with u_noise_amp = 0.5 K on one rank) ----------
+
+def test_noise_field_is_glibc_rand_from_seed_1():
+    """the reference's noise field (equation.c:450-456, rand() never seeded by the harness) is
+    amp (rand()/RAND_MAX - 0.5) of glibc's sequence from seed 1, node by node in [k][j][i] order --
+    what libpft draws after srand(1) (intertrack_model.c PrecalculateData)"""
+    meta, A = O.load_case("gnoise")
+    noise = O.glibc_noise(meta["u_noise_amp"], A["noise"].size)
+    assert np.abs(A["noise"]).max() > 0.2
+    assert np.array_equal(noise.reshape(A["noise"].shape), A["noise"])
+
+
+@pytest.mark.parametrize("mode", [0, 10, 1, 11])
+def test_noise_rhs_equals_reference(mode):
+    """the four models that add u_noise to u in their reaction term (equation.c:676, 687), at a
+    state with mixed phases"""
+    meta, A = O.load_case("gnoise")
+    P, info = O.params_from_meta({"params": meta[f"m{mode}_params"]})
+    assert info["calc_mode"] == mode and P[O.PARAM_NAMES.index("u_noise_amp")] == meta["u_noise_amp"]
+    x, t = A[meta["rhs_state"]], meta["rhs_time"]
+    K, _ = O.rhs(info, P, mode, t, x, noise=A["noise"])
+    assert np.array_equal(K, A[f"rhs_m{mode}"])
+    K0, _ = O.rhs(info, P, mode, t, x)
+    assert not np.array_equal(K0, A[f"rhs_m{mode}"])        # the noise is seen
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_noise_trajectory_equals_reference(mode):
+    meta, A = O.load_case("gnoise")
+    P, info = O.params_from_meta({"params": meta[f"m{mode}_params"]})
+    res = O.solve(info, P, mode, A["ic"], 0.0, 1.0, meta["traj_times"], noise=A["noise"])
+    for i, (t, h, s, st, rc, x) in enumerate(res):
+        ref = meta[f"traj_m{mode}"][i]
+        assert (t.hex(), h.hex(), s, st, rc) == (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(),
+                                                 ref[2], ref[3], ref[4])
+        assert np.array_equal(x, A[f"traj_m{mode}_state{i}"])
