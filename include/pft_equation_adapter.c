@@ -24,6 +24,9 @@
  *     communicator is in virtual order, where the master is always 0;
  *   - RK_MPI_SA_cleanup() also releases the communicator.
  */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 #include "pft_model.h"
 #include "pft_solver.h"
 #include "pft_comm.h"
@@ -38,14 +41,40 @@ static pft_comm * pft_adapter_comm = NULL;
 
 static int pft_adapter_comm_init(void)
 {
-	char uid[128];
-	int ndev = 1;
+	/* [0]: the master's status, [1..128]: the RCCL unique id.  The master broadcasts even when it
+	   has no id, and every rank agrees that it has a device before the (collective, blocking) RCCL
+	   init: a rank that cannot take part makes all of them fail here, as the driver's
+	   CheckErrorAcrossRanks after AllocPrecalcData (intertrack.c:1814-1826) expects, instead of
+	   leaving the others blocked in MPI_Bcast or ncclCommInitRank. */
+	char msg[1 + 128];
+	int ndev = 0, ok = 0, i;
 	if(MPIprocs == 1) return pft_comm_init_self(&pft_adapter_comm) ? 1 : 0;
-	if(MPIrank == 0 && pft_comm_get_unique_id(uid)) return 1;
-	MPI_Bcast(uid, (int)sizeof(uid), MPI_BYTE, MPIrankmap[0], MPI_COMM_WORLD);
-	if(pft_hip_device_count(&ndev) || ndev < 1) return 1;
+	memset(msg, 0, sizeof(msg));
+#ifdef PFT_ADAPTER_TEST_UID
+	/* test hook (tests/test_adapter.py runs the driver on CPU-only hosts, where RCCL has no id) */
+	if(MPIrank == 0) { for(i = 0; i < 128; i++) msg[1 + i] = (char)(i * 37 + 11); msg[0] = 1; }
+#else
+	if(MPIrank == 0) msg[0] = pft_comm_get_unique_id(msg + 1) == 0;
+#endif
+	MPI_Bcast(msg, (int)sizeof(msg), MPI_BYTE, MPIrankmap[0], MPI_COMM_WORLD);
+	if(getenv("PFT_ADAPTER_TRACE")) {
+		unsigned long h = 5381;
+		for(i = 1; i <= 128; i++) h = h * 33 + (unsigned char)msg[i];
+		fprintf(stderr, "pft_adapter: rank %d of %d: master status %d, unique id digest %016lx\n", MPIrank,
+		        MPIprocs, msg[0], h);
+	}
+	if(!msg[0]) {
+		fprintf(stderr, "pft_adapter: rank %d: the master has no RCCL unique id (%s)\n", MPIrank, pft_hip_last_error());
+		return 1;
+	}
+	ok = pft_hip_device_count(&ndev) == 0 && ndev >= 1;
+	MPI_Allreduce(MPI_IN_PLACE, &ok, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
+	if(!ok) {
+		fprintf(stderr, "pft_adapter: rank %d: no HIP device on %s rank\n", MPIrank, ndev >= 1 ? "another" : "this");
+		return 1;
+	}
 	/* one process per GPU, ranks packed per node */
-	if(pft_comm_init_rccl(&pft_adapter_comm, MPIprocs, MPIrank, uid, MPIrank % ndev)) return 1;
+	if(pft_comm_init_rccl(&pft_adapter_comm, MPIprocs, MPIrank, msg + 1, MPIrank % ndev)) return 1;
 	return pft_comm_set_current(pft_adapter_comm) ? 1 : 0;
 }
 

@@ -58,7 +58,17 @@ int main(int argc, char ** argv)
 	N1 = n1 + 2 * bcond_thickness; N2 = n2 + 2 * bcond_thickness; N3 = n3 + 2 * bcond_thickness;
 	S = (long)N1 * N2 * N3;
 	solution = (FLOAT *)calloc(3 * S, sizeof(FLOAT));
-	if(!solution || AllocPrecalcData()) { fprintf(stderr, "AllocPrecalcData failed\n"); MPI_Abort(MPI_COMM_WORLD, 4); }
+	{
+		/* the driver's CheckErrorAcrossRanks (intertrack.c:1814-1826): every rank learns of any
+		   rank's allocation error and all of them exit */
+		int err = !solution || AllocPrecalcData(), any = 0;
+		MPI_Allreduce(&err, &any, 1, MPI_INT, MPI_MAX, MPI_COMM_WORLD);
+		if(any) {
+			if(err) fprintf(stderr, "rank %d: AllocPrecalcData failed\n", MPIrank);
+			MPI_Finalize();
+			return 4;
+		}
+	}
 	if(pft_model_ic_default(solution)) MPI_Abort(MPI_COMM_WORLD, 5);
 	if(PrecalculateData(var_eps_mult)) { fprintf(stderr, "PrecalculateData failed\n"); MPI_Abort(MPI_COMM_WORLD, 6); }
 

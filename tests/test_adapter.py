@@ -21,14 +21,14 @@ LIBDIR = os.path.join(REPO, "porousfreezethaw_amd", "lib")
 MPI_INC, MPI_LIB = "/opt/conda/include", "/opt/conda/lib"
 
 
-def _build(tmp):
+def _build(tmp, extra=()):
     if not os.path.exists(os.path.join(MPI_INC, "mpi.h")):
         pytest.skip("no MPI headers in this image")
     if not os.path.exists(os.path.join(LIBDIR, "libpft.so")):
         pytest.skip("libpft not built")
-    exe = os.path.join(tmp, "mock_intertrack")
+    exe = os.path.join(tmp, "mock_intertrack" + "".join(e.replace("-D", "_") for e in extra))
     # the system libstdc++ must win over the MPI distribution's older copy (ROCm needs it)
-    cmd = ["gcc", "-std=c99", "-O2", "-Wall", "-Werror", "-Wno-unused-variable", "-DPFT_USE_MPI",
+    cmd = ["gcc", "-std=c99", "-O2", "-Wall", "-Werror", "-Wno-unused-variable", "-DPFT_USE_MPI", *extra,
            f"-I{MPI_INC}", f"-I{os.path.join(REPO, 'include')}", SRC, f"-L{LIBDIR}", "-lpft",
            os.path.join(MPI_LIB, "libmpi.so"),
            f"-Wl,-rpath,{LIBDIR}:/usr/lib/x86_64-linux-gnu:{MPI_LIB}", "-o", exe]
@@ -39,6 +39,56 @@ def _build(tmp):
 
 def test_adapter_compiles_into_driver(tmp_path):
     _build(str(tmp_path))
+
+
+MPIRUN = "/opt/conda/bin/mpirun"
+
+
+def _driver_args(exe, tmp_path):
+    meta, A = O.load_case("g20")
+    P, info = O.params_from_meta(meta)
+    (tmp_path / "params.txt").write_text("".join(float(v).hex() + "\n" for v in P))
+    (tmp_path / "data").mkdir(exist_ok=True)
+    (tmp_path / "data" / "spheres_positions.txt").write_text(
+        "".join("%.17g %.17g %.17g\n" % tuple(b) for b in O.beads()))
+    h = lambda v: float(v).hex()  # noqa: E731
+    return [exe, "params.txt", str(info["n1"]), str(info["n2"]), str(info["n3"]), h(info["L1"]),
+            h(info["L2"]), h(info["L3"]), "0", h(1.0), h(info["tau_min"]), h(info["delta"]),
+            h(meta["traj_times"][0]), "out.bin"]
+
+
+@pytest.mark.parametrize("test_uid", [True, False])
+def test_adapter_multirank_without_device_fails_cleanly(tmp_path, test_uid):
+    """The adapter's multi-rank branch (pft_equation_adapter.c: the RCCL unique id broadcast over the
+    driver's MPI_COMM_WORLD) under `mpirun -np 2` on a host without a GPU: with a fixed id from the
+    master (test hook) both ranks receive the same 128 bytes, then agree that a rank has no device
+    and fail -- the driver's AllocPrecalcData error -- instead of blocking in RCCL's init; without
+    the hook RCCL gives the master no id, which every rank learns from the broadcast.  Either way
+    the run ends, well within the timeout."""
+    import glob
+    if not os.path.exists(MPIRUN):
+        pytest.skip("no mpirun in this image")
+    import porousfreezethaw_amd as PA
+    if PA.device_count() > 0:
+        pytest.skip("a GPU is visible: this test covers the no-device failure path")
+    exe = _build(str(tmp_path), ("-DPFT_ADAPTER_TEST_UID",) if test_uid else ())
+    env = dict(os.environ, PFT_ADAPTER_TRACE="1", OMP_NUM_THREADS="1")
+    r = subprocess.run([MPIRUN, "-np", "2"] + _driver_args(exe, tmp_path), cwd=tmp_path, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+    trace = [l for l in r.stderr.splitlines() if "unique id digest" in l]
+    assert len(trace) == 2, r.stderr
+    digests = {l.split()[-1] for l in trace}
+    assert len(digests) == 1                                   # the same 128 bytes on both ranks
+    status = {l.split("master status")[1].split(",")[0].strip() for l in trace}
+    if test_uid:
+        assert status == {"1"}
+        assert sum("no HIP device" in l for l in r.stderr.splitlines()) == 2, r.stderr
+    else:
+        assert status == {"0"}
+        assert sum("has no RCCL unique id" in l for l in r.stderr.splitlines()) == 2, r.stderr
+    assert "AllocPrecalcData failed" in r.stderr
+    assert not glob.glob(str(tmp_path / "out.bin"))
 
 
 @pytest.mark.gpu
