@@ -209,7 +209,7 @@ int pft_slab_book_load(pft_slab * s, int which);
    launch.  Stage A's K is evaluated on the tile and a one-cell ring and never stored; stage B
    writes K3 (first = 2) or the error norm and x(t+h) into XN (first = 4), bit for bit what the
    two stage launches give.  t_a / t_b: the two stage times (Dirichlet value); h: the step; coef:
-   h3 for x(t+h).  set_pair: 0 off, 1 (default) automatic (slabs of >= 16 Ki cells per CU), 2 on
+   h3 for x(t+h).  set_pair: 0 off, 1 (default) automatic (slabs of >= 4 Ki cells per CU), 2 on
    any slab they fit; env PFT_PAIR=0/1/2 overrides.  pair_ok: 1 when this slab runs them (even
    n1, no z-neighbours, the mode allows); pair_geometry: the tile (tx cells x ty rows) */
 int pft_slab_set_pair(pft_slab * s, int on);

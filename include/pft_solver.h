@@ -70,7 +70,7 @@ enum {
 	PFT_OPT_PAIR = 10       /* stages 2+3 and 4+5 as pair kernels (pft_slab_pair: stage A evaluated
 	                           inside stage B's stencil, never stored -- 21 instead of 39 doubles
 	                           per cell-step, bit-identical): 1 (default) = on slabs of at least
-	                           16 Ki cells per CU (4 M cells on MI355X), 2 = on any slab they fit,
+	                           4 Ki cells per CU (1 M cells on MI355X), 2 = on any slab they fit,
 	                           0 = one launch per stage */
 	,
 	PFT_OPT_FAIL_RHS = 11,  /* test hook: N > 0 makes the N-th device evaluation of libpft's own

@@ -238,8 +238,9 @@ class Simulation:
                 rc = L_.pft_ic_eval(C.byref(self.grid), q, len(prog), _ip(ops), _dp(args), _dp(self.x))
                 if rc:
                     raise ValueError(f"pft_ic_eval failed ({rc})")
-        elif initial is None and not device_ic:
-            L_.pft_model_ic_default(_dp(self.x))
+        elif initial is None:
+            if not device_ic:   # (device_ic: computed on the device below, then downloaded)
+                L_.pft_model_ic_default(_dp(self.x))
         else:
             self.set_interior(initial)
         nch = 3 * g.n2 * g.n3

@@ -1067,11 +1067,12 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
 #define PFT_PAIR_PADP 2         // slots before / after the positions of each half: the discarded
                                 // outer cell of a ring pair reads one slot beyond its row
 #define PFT_PAIR_H 512          // doubles per half (even / odd cells) of a field plane
+#define PFT_PAIR_HB 468         // slots of a stage-B plane in the interleaved layout (rows 1..ty+2)
 // The row pitch LWP (pairs) is a template parameter, a compile-time constant so that every LDS
 // access is a per-lane base + an immediate offset: 22 (tiles up to 40 cells wide, 19 rows) or 12
 // (up to 20 cells wide, 38 rows: n1 = 100 in 5 tiles of 20 where 40-wide tiles leave a sixth idle)
 #ifndef PFT_PAIR_MIN_CELLS_PER_CU
-#define PFT_PAIR_MIN_CELLS_PER_CU 16384
+#define PFT_PAIR_MIN_CELLS_PER_CU 4096
 #endif
 
 struct PairArgs {
@@ -1202,52 +1203,64 @@ __device__ __forceinline__ dbl2 pair_in_B(const PairArgs& a, int q, const PairRa
   return v;
 }
 
-// a pair from / to the LDS halves at slot p, with its cells exchanged when sw = 1 (two 8-byte
-// accesses at per-lane offsets)
-#ifndef PFT_PAIR_SWSEL
-#define PFT_PAIR_SWSEL 1
+// A pair from / to LDS at position slot p, with its cells exchanged when sw = 1 (two 8-byte
+// accesses at per-lane offsets).  Two layouts of a field plane (EO, a template parameter):
+//   EO = true : the even cells of the positions in one half, the odd cells PFT_PAIR_H doubles
+//               later (slot p: doubles p and PFT_PAIR_H + p) -- no bank conflicts;
+//   EO = false: the cells of a position side by side (slot p: doubles 2p, 2p + 1) -- 2-way bank
+//               conflicts (16-byte lane stride), but a mirrored lane's two accesses share a base.
+// Measured (A/B, one box, 400^3): pair 2+3 0.358 ms with EO against 0.362-0.365 interleaved;
+// pair 4+5 0.410-0.415 interleaved against 0.416-0.424 with EO (profiles/r04b_ab_pair_lds.txt):
+// the defaults below (PFT_PAIR_EO_MASK bit 0: pair 2+3, bit 1: pair 4+5).
+#ifndef PFT_PAIR_EO_MASK
+#define PFT_PAIR_EO_MASK 1
 #endif
-__device__ __forceinline__ dbl2 ldeo(const double* L, int p, int sw)
-{
-  dbl2 v;
-#if PFT_PAIR_SWSEL
-  const double e = L[p], o = L[PFT_PAIR_H + p];
-  v.x = sw ? o : e;
-  v.y = sw ? e : o;
-#else
-  v.x = L[sw * PFT_PAIR_H + p];
-  v.y = L[(1 - sw) * PFT_PAIR_H + p];
-#endif
-  return v;
-}
-__device__ __forceinline__ void steo(double* L, int p, dbl2 v, int sw)
-{
-#if PFT_PAIR_SWSEL
-  L[p] = sw ? v.y : v.x;
-  L[PFT_PAIR_H + p] = sw ? v.x : v.y;
-#else
-  L[sw * PFT_PAIR_H + p] = v.x;
-  L[(1 - sw) * PFT_PAIR_H + p] = v.y;
-#endif
-}
-__device__ __forceinline__ dbl2 ldeo(const double* L, int p) { return dbl2{L[p], L[PFT_PAIR_H + p]}; }
-__device__ __forceinline__ void steo(double* L, int p, dbl2 v)
-{
-  L[p] = v.x;
-  L[PFT_PAIR_H + p] = v.y;
-}
+template <bool EO>
+struct PairLds;
+template <>
+struct PairLds<true> {
+  static constexpr int H = PFT_PAIR_H;
+  __device__ static __forceinline__ dbl2 ld(const double* L, int p, int sw)
+  {
+    return dbl2{L[sw * H + p], L[(1 - sw) * H + p]};
+  }
+  __device__ static __forceinline__ void st(double* L, int p, dbl2 v, int sw)
+  {
+    L[sw * H + p] = v.x;
+    L[(1 - sw) * H + p] = v.y;
+  }
+  __device__ static __forceinline__ dbl2 ld(const double* L, int p) { return dbl2{L[p], L[H + p]}; }
+  __device__ static __forceinline__ void st(double* L, int p, dbl2 v)
+  {
+    L[p] = v.x;
+    L[H + p] = v.y;
+  }
+  __device__ static __forceinline__ double cell(const double* L, int p, int s) { return L[s * H + p]; }   // cell s of slot p
+};
+template <>
+struct PairLds<false> {
+  __device__ static __forceinline__ dbl2 ld(const double* L, int p, int sw)
+  {
+    const double* q = L + 2 * p;
+    return dbl2{q[sw], q[1 - sw]};
+  }
+  __device__ static __forceinline__ void st(double* L, int p, dbl2 v, int sw) { st2x(L + 2 * p, v, sw); }
+  __device__ static __forceinline__ dbl2 ld(const double* L, int p) { return ld2(L + 2 * p); }
+  __device__ static __forceinline__ void st(double* L, int p, dbl2 v) { st2(L + 2 * p, v); }
+  __device__ static __forceinline__ double cell(const double* L, int p, int s) { return L[2 * p + s]; }
+};
 
 // the RHS of one cell pair (du, dp of both cells): centre zc, z neighbours zm / zp, x/y
 // neighbours from the LDS field planes L[q] around slot p (even / odd halves, row pitch LWP); the
 // x-face between the pair's cells is evaluated once and the z-face below is carried in fz
 // (rhs_cell_f, bit-exact), as in merson_fused
-template <int MODE, int LWP>
+template <int MODE, int LWP, bool EO>
 __device__ __forceinline__ void pair_rhs(const pft_consts& c, const double* L0, const double* L1, const double* L2,
                                          int p, const dbl2* zm, const dbl2* zc, const dbl2* zp,
                                          const double* nz, FaceT* fz, double* du, double* dp)
 {
   constexpr bool FLUX = MODE != 10 && MODE != 11;
-  constexpr int H = PFT_PAIR_H;
+  using LD = PairLds<EO>;
   const double* L[3] = {L0, L1, L2};
   FaceT fx;
 #pragma unroll
@@ -1257,10 +1270,10 @@ __device__ __forceinline__ void pair_rhs(const pft_consts& c, const double* L0, 
     for (int q = 0; q < 3; ++q) {
       const double cen = zc[q][s];
       col[q].c = cen;
-      col[q].xm = s == 0 ? L[q][H + p - 1] : zc[q][0];     // odd cell of the pair to the left
-      col[q].xp = s == 0 ? zc[q][1] : L[q][p + 1];         // even cell of the pair to the right
-      col[q].ym = L[q][s * H + p - LWP];
-      col[q].yp = L[q][s * H + p + LWP];
+      col[q].xm = s == 0 ? LD::cell(L[q], p - 1, 1) : zc[q][0];   // odd cell of the pair to the left
+      col[q].xp = s == 0 ? zc[q][1] : LD::cell(L[q], p + 1, 0);   // even cell of the pair to the right
+      col[q].ym = LD::cell(L[q], p - LWP, s);
+      col[q].yp = LD::cell(L[q], p + LWP, s);
       col[q].zm = zm[q][s];
       col[q].zp = zp[q][s];
     }
@@ -1282,11 +1295,15 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
 {
   constexpr bool FLUX = MODE != 10 && MODE != 11;
   constexpr dbl2 zero2 = {0.0, 0.0};
+  constexpr bool EO = (PFT_PAIR_EO_MASK >> (SA == 2 ? 0 : 1)) & 1;
+  using LD = PairLds<EO>;
 #if defined(__HIP_DEVICE_COMPILE__)
   const pft_kptr kbase = (pft_kptr)__builtin_amdgcn_kernarg_segment_ptr();
 #endif
+  // (the interleaved layout's stage-B ring holds rows 1..ty+2 only: PFT_PAIR_HB slots, no padding
+  // to the halves -- its LDS offsets, and with them the registers the kernel needs, as in round 3)
   __shared__ __attribute__((aligned(16))) double lA[3][3][2 * PFT_PAIR_H];
-  __shared__ __attribute__((aligned(16))) double lB[3][3][2 * PFT_PAIR_H];
+  __shared__ __attribute__((aligned(16))) double lB[3][3][EO ? 2 * PFT_PAIR_H : 2 * PFT_PAIR_HB];
 
   const int TX = a.tx, TY = a.ty, WP2 = TX / 2 + 2, NPOS = WP2 * (TY + 4);
   const int lin = xcd_remap(blockIdx.x, a.ntile * a.nchunk);
@@ -1345,18 +1362,18 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         iam[q] = pair_in_A<SA, GLX>(a, q, t);
-        steo(lA[2][q], posA, iam[q], xsw);
+        LD::st(lA[2][q], posA, iam[q], xsw);
       }
     }
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       ia0[q] = pair_in_A<SA, GLX>(a, q, R[0]);
-      steo(lA[0][q], posA, ia0[q], xsw);
+      LD::st(lA[0][q], posA, ia0[q], xsw);
       if (mA0 == mfirst) {
         // bottom wall: plane -1 mirrors plane 0 (equation.c:164-174), also in the ring slot of
         // plane -1, so that the z-loop reads its z neighbours without selects
         iam[q] = ia0[q];
-        steo(lA[2][q], posA, ia0[q], xsw);
+        LD::st(lA[2][q], posA, ia0[q], xsw);
       }
     }
 #pragma unroll
@@ -1381,7 +1398,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
       // placement lost track of them and stage A waited for the look-ahead it had just issued.
       if (mm + 1 <= mlast) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) steo(lA[sAp][q], posA, pair_in_A<SA, GLX>(A0, q, rn), xsw);
+        for (int q = 0; q < 3; ++q) LD::st(lA[sAp][q], posA, pair_in_A<SA, GLX>(A0, q, rn), xsw);
       }
       if (mm + 2 <= mlast) pair_load<SA>(A0, pbo(mm + 2), rnn);          // look-ahead
     }
@@ -1403,26 +1420,26 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
           // top wall: the ring slot of plane n3 holds the ghost values -- Dirichlet u (equation.c:
           // 175-183), p and gl mirrored -- at this position (its own z neighbour only)
 #pragma unroll
-          for (int q = 1; q < 3; ++q) steo(lA[sAp][q], posA, ldeo(lA[sA][q], posA));
-          steo(lA[sAp][0], posA, dbl2{A1.T_topA, A1.T_topA});
+          for (int q = 1; q < 3; ++q) LD::st(lA[sAp][q], posA, LD::ld(lA[sA][q], posA));
+          LD::st(lA[sAp][0], posA, dbl2{A1.T_topA, A1.T_topA});
         }
         dbl2 zc[3], zm[3], zp[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          zc[q] = ldeo(lA[sA][q], posA, xsw);
-          zm[q] = ldeo(lA[sAm][q], posA, xsw);
-          zp[q] = ldeo(lA[sAp][q], posA, xsw);
+          zc[q] = LD::ld(lA[sA][q], posA, xsw);
+          zm[q] = LD::ld(lA[sAm][q], posA, xsw);
+          zp[q] = LD::ld(lA[sAp][q], posA, xsw);
         }
         double du[2], dp[2];
         const double* nz = A1.noise ? A1.noise + (long)mm * A1.plane + (long)apo : nullptr;
-        pair_rhs<MODE, LWP>(C1, lA[sA][0], lA[sA][1], lA[sA][2], actA, zm, zc, zp, nz, fzA, du, dp);
+        pair_rhs<MODE, LWP, EO>(C1, lA[sA][0], lA[sA][1], lA[sA][2], actA, zm, zc, zp, nz, fzA, du, dp);
         ka[0] = dbl2{du[0], du[1]};
         ka[1] = dbl2{dp[0], dp[1]};
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
           const dbl2 ib = pair_in_B<SA, GLX>(A1, q, rc, q < 2 ? ka[q < 2 ? q : 0] : zero2);
-          steo(lB[sA][q], posB, ib, xsw);
-          if (mm == 0 && wlo) steo(lB[sAm][q], posB, ib, xsw);   // bottom wall: plane -1 mirrors plane 0
+          LD::st(lB[sA][q], posB, ib, xsw);
+          if (mm == 0 && wlo) LD::st(lB[sAm][q], posB, ib, xsw);   // bottom wall: plane -1 mirrors plane 0
         }
       }
     }
@@ -1447,15 +1464,15 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
         if (kB == n3 - 1 && whi) {
           // top wall: the ghost values of plane n3 at this position (as in stage A above)
 #pragma unroll
-          for (int q = 1; q < 3; ++q) steo(lB[sBp][q], lo, ldeo(lB[sB][q], lo));
-          steo(lB[sBp][0], lo, dbl2{A2.T_topB, A2.T_topB});
+          for (int q = 1; q < 3; ++q) LD::st(lB[sBp][q], lo, LD::ld(lB[sB][q], lo));
+          LD::st(lB[sBp][0], lo, dbl2{A2.T_topB, A2.T_topB});
         }
         dbl2 zc[3], zm[3], zp[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          zc[q] = ldeo(lB[sB][q], lo);
-          zm[q] = ldeo(lB[sBm][q], lo);
-          zp[q] = ldeo(lB[sBp][q], lo);
+          zc[q] = LD::ld(lB[sB][q], lo);
+          zm[q] = LD::ld(lB[sBm][q], lo);
+          zp[q] = LD::ld(lB[sBp][q], lo);
         }
         if (kB == kb) {
           // the z-face below the chunk's first stage-B plane
@@ -1466,7 +1483,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
         double du[2], dp[2];
         const unsigned e0 = pbo(kB);
         const double* nz = A2.noise ? A2.noise + (long)kB * A2.plane + (long)apo : nullptr;
-        pair_rhs<MODE, LWP>(C2, lB[sB][0], lB[sB][1], lB[sB][2], lo, zm, zc, zp, nz, fzB, du, dp);
+        pair_rhs<MODE, LWP, EO>(C2, lB[sB][0], lB[sB][1], lB[sB][2], lo, zm, zc, zp, nz, fzB, du, dp);
         if (SA == 2) {
           stb(A2.out, e0, dbl2{du[0], du[1]});                   // K3 (hybrid2.c:412-429)
           stb(A2.out + A2.fs, e0, dbl2{dp[0], dp[1]});
@@ -3000,7 +3017,7 @@ static bool pair_geometry_ok(int tx, int ty)
 {
   const int lwp = pair_lwp(tx);
   return tx >= 2 && tx % 2 == 0 && ty >= 1 && (tx / 2 + 2) * (ty + 4) <= PFT_PBLOCK && tx / 2 + 2 <= 22 &&
-         2 * PFT_PAIR_PADP + lwp * (ty + 4) <= PFT_PAIR_H;
+         2 * PFT_PAIR_PADP + lwp * (ty + 4) <= PFT_PAIR_H && 2 * PFT_PAIR_PADP + lwp * (ty + 2) <= PFT_PAIR_HB;
 }
 
 // automatic tile: the fewest workgroups per plane (a workgroup-plane costs about the same whatever
@@ -3152,9 +3169,9 @@ int pft_slab_set_pair(pft_slab* s, int on)
 int pft_slab_pair_ok(const pft_slab* s)
 {
   // automatic: slabs of at least PFT_PAIR_MIN_CELLS_PER_CU cells per CU.  Measured (A/B, one box):
-  // 400^3 +8..14%, the 800^3 8-way rank slab +8..12%, the 64 M-cell cube +18%, but 200^3 (2 M
-  // cells) -3.5% and 100^3 -4.5%, where the chunks' extra stage-A planes and the launch latency
-  // of fewer, longer workgroups dominate
+  // 400^3 +28% (round 3), 200^3 (2 M cells, 7.8 Ki per CU) +6% since the 12-pair row pitch of
+  // 100-wide planes (round 4: 14 384 against 13 575 Mcells*steps/s), 100^3 -28% (one workgroup
+  // per CU marching 3-5 planes, two of them stage-A-only, against one plane per workgroup)
   if (s->pair_on == 1 && (double)s->plane * s->d.n3 < (double)s->n_cu * PFT_PAIR_MIN_CELLS_PER_CU) return 0;
   // z-neighbours: the two-plane halo (pft_comm_halo_deep) needs n3 >= 2, and stage A on a ghost
   // plane would need the neighbour's u_noise there (not exchanged: one launch per stage then)

@@ -113,32 +113,37 @@ def _golden_sim(meta, mode, **kw):
     return sim
 
 
-@pytest.mark.parametrize("case,mode", [("g200", 0), ("g200", 1), ("g400", 0)])
-def test_full_size_reference_trajectory_bitwise(case, mode):
+@pytest.mark.parametrize("case,mode,pair", [("g200", 0, 1), ("g200", 1, 1), ("g200", 0, 0), ("g400", 0, 1)])
+def test_full_size_reference_trajectory_bitwise(case, mode, pair):
     """RK_MPI_SA_solve on the MI355X to the reference's own snapshot times at BASELINE sizes: t, h,
     step counts, return code and every field bit for bit (tests/golden/g200, g400: the reference
-    compiled in place, run on 8 MPI ranks and re-checked on 3 / 5)"""
+    compiled in place, run on 8 MPI ranks and re-checked on 3 / 5); pair 1: the automatic choice
+    (the pair kernels at both sizes), 0: one launch per stage"""
     meta, A = O.load_case(case)
-    sim = _golden_sim(meta, mode)
-    for i, T in enumerate(meta[f"traj_m{mode}_times"]):
-        rc = sim.solve(T)
-        _check_golden(meta, A, mode, i, (sim.t, sim.h, sim.system.steps, sim.system.steps_total, rc),
-                      sim.interior())
-    st = sim.stats()
+    L = P.lib()
+    L.pft_solver_set_option(P.PFT_OPT_PAIR, pair)
+    try:
+        sim = _golden_sim(meta, mode)
+        for i, T in enumerate(meta[f"traj_m{mode}_times"]):
+            rc = sim.solve(T)
+            _check_golden(meta, A, mode, i, (sim.t, sim.h, sim.system.steps, sim.system.steps_total, rc),
+                          sim.interior())
+        st = sim.stats()
+        sim.close()
+    finally:
+        L.pft_solver_set_option(P.PFT_OPT_PAIR, 1)
     assert st.path == 1
     assert sim.system.steps < sim.system.steps_total           # rejected steps in the window
-    if case == "g400":
-        assert st.pairs == 1                                   # the benchmark's pair kernels
-    sim.close()
+    assert st.pairs == pair                                    # the benchmark's pair kernels, or not
 
 
-@pytest.mark.parametrize("pair", [1, 2])
+@pytest.mark.parametrize("pair", [0, 1])
 def test_400_four_slabs_reach_the_reference(pair):
     """configs[3]: 400^3 split 4-way (4 x 100 planes, loopback transport), RK_MPI_SA_solve to the
     reference's g400 snapshot times (~45 and 67 attempted steps): every slab's t, h, counts and the
-    assembled fields equal the reference's bit for bit.  pair 1: the automatic choice (a 4 M-cell
-    slab is below the pair kernels' threshold: one launch per stage, boundary planes first); 2: the
-    pair kernels forced, with the two-plane halo exchanged beside the interior launch"""
+    assembled fields equal the reference's bit for bit.  pair 0: one launch per stage, boundary
+    planes first; 1: the automatic choice (a 4 M-cell slab is above the pair kernels' threshold:
+    the pair kernels, with the two-plane halo exchanged beside the interior launch)"""
     meta, A = O.load_case("g400")
     Pm, info = O.params_from_meta({"params": meta["m0_params"]})
     times = meta["traj_m0_times"]
@@ -159,7 +164,7 @@ def test_400_four_slabs_reach_the_reference(pair):
 
     out = M.loopback_run(4, make, run)
     assert [o[2] for o in out] == [100] * 4
-    assert all(o[3] == (pair == 2) for o in out)
+    assert all(o[3] == (pair == 1) for o in out)
     for i in range(len(times)):
         assert all(o[0][i] == out[0][0][i] for o in out)
         _check_golden(meta, A, 0, i, out[0][0][i], np.concatenate([o[1][i] for o in out], axis=1))
