@@ -263,7 +263,12 @@ int pft_probe_copy(double * dst, const double * src, size_t n, void * stream);
    kernel-to-kernel hand-off on one GPU, whatever the receiving L2s held of the ghost planes. */
 #define PFT_IPC_HANDLE_BYTES (64 * (PFT_BUF_COUNT + 2))
 int pft_slab_ipc_export(pft_slab * s, void * handles);
-int pft_slab_ipc_set_peer(pft_slab * s, int side, const void * handles, int n3, long fs, int device);
+/* 1 when this process asks for staged receive between processes on one GPU (env PFT_IPC_STAGED=1) */
+int pft_ipc_staged_env(void);
+/* peer_staged: the neighbour's own staged-receive choice (its PFT_IPC_STAGED, published at attach);
+   both ends of a link stage when either asks for it, or when the neighbour is on another GPU */
+int pft_slab_ipc_set_peer(pft_slab * s, int side, const void * handles, int n3, long fs, int device,
+                          int peer_staged);
 int pft_slab_ipc_close(pft_slab * s);
 int pft_slab_halo_put(pft_slab * s, int role, int f0, int f1, unsigned long long seq);
 /* the same with deep = 1: also planes 2 and n3-1 into the neighbours' far ghost planes (the pair

@@ -34,6 +34,7 @@ enum { KIND_SELF = 0, KIND_RCCL = 1, KIND_LOOP = 2, KIND_IPC = 3 };
 
 struct IpcSlot {              // one rank's slab, published at attach
   int n3, device;
+  int staged;                 // its staged-receive request (PFT_IPC_STAGED): both ends of a link agree
   long fs;
   char handles[PFT_IPC_HANDLE_BYTES];
 };
@@ -372,18 +373,19 @@ static int ipc_attach(pft_comm* c, pft_slab* s)
   me->n3 = pft_slab_nz(s);
   me->device = c->device;
   me->fs = (long)pft_slab_field_stride(s);
+  me->staged = pft_ipc_staged_env();
   if ((rc = ipc_round(c, nullptr, 0, nullptr, 0, &recs))) return rc;   // every slot is published
   if (c->self_x) {
-    if ((rc = pft_slab_ipc_set_peer(s, 0, nullptr, 0, 0, 0)) || (rc = pft_slab_ipc_set_peer(s, 1, nullptr, 0, 0, 0)))
+    if ((rc = pft_slab_ipc_set_peer(s, 0, nullptr, 0, 0, 0, 0)) || (rc = pft_slab_ipc_set_peer(s, 1, nullptr, 0, 0, 0, 0)))
       return rc;
   } else {
     if (c->rank > 0) {
       const IpcSlot* b = &c->shm->slot[c->rank - 1];
-      if ((rc = pft_slab_ipc_set_peer(s, 0, b->handles, b->n3, b->fs, b->device))) return rc;
+      if ((rc = pft_slab_ipc_set_peer(s, 0, b->handles, b->n3, b->fs, b->device, b->staged))) return rc;
     }
     if (c->rank < c->size - 1) {
       const IpcSlot* a = &c->shm->slot[c->rank + 1];
-      if ((rc = pft_slab_ipc_set_peer(s, 1, a->handles, a->n3, a->fs, a->device))) return rc;
+      if ((rc = pft_slab_ipc_set_peer(s, 1, a->handles, a->n3, a->fs, a->device, a->staged))) return rc;
     }
   }
   // the slots are reused by the next attach only after everyone has read them

@@ -252,6 +252,9 @@ struct StageArgs {
   unsigned long long gdec_seq;
   double dt, dh, d_final, d_delta, d_hmin;
   int d_local, d_nan;
+  int d_flip;          // test hook (env PFT_GATE_FLIP = N): every N-th accepted decision leaves the
+                       // device with the last bit of its h flipped, so the host's check must discard
+                       // and relaunch that step (tests/test_gate_gpu.py)
 };
 
 #define PFT_GATE_SKIP (1ULL << 63)
@@ -345,6 +348,7 @@ __device__ __forceinline__ void gate_decide(const StageArgs& a, double t, double
       const double hn = (fabs(a.d_final - tn) <= fabs(new_h)) ? a.d_final - tn : new_h;   // :743-761
       tb = (unsigned long long)__double_as_longlong(tn);
       hb = (unsigned long long)__double_as_longlong(hn);
+      if (a.d_flip > 0 && a.gdec_seq % (unsigned long long)a.d_flip == 0) hb ^= 1ULL;
       v = a.gdec_seq;
     }
   }
@@ -1890,6 +1894,7 @@ struct pft_slab {
   unsigned long long gate_use_seq;   // launches enqueued now are gated on this decision (0: not)
   double gate_final, gate_delta, gate_hmin;   // the solve's constants (pft_slab_gate_config)
   int gate_local, gate_nan;
+  int gate_flip;         // test hook, env PFT_GATE_FLIP (StageArgs::d_flip)
   // eps-publication bookkeeping snapshots (pft_slab_book_save/load): the launches of the next
   // step are enqueued between this step's launches and the read of its error norm
   struct Book {
@@ -2036,6 +2041,8 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
     s->pair_env = ep != nullptr;
     s->pair_on = ep ? atoi(ep) : 1;
     s->pair_ntile = pair_geometry(d->n1, d->n2, &s->pair_tx, &s->pair_ty);
+    const char* eg = getenv("PFT_GATE_FLIP");
+    s->gate_flip = eg ? atoi(eg) : 0;
     const char* et = getenv("PFT_IPC_TIMEOUT");
     s->timeout_s = (et && atof(et) > 0.0) ? atof(et) : 300.0;
   }
@@ -2566,6 +2573,7 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
     a.d_hmin = s->gate_hmin;
     a.d_local = s->gate_local;
     a.d_nan = s->gate_nan;
+    a.d_flip = s->gate_flip;
     __atomic_store_n(&s->gate_pin[4 * j], 0ULL, __ATOMIC_RELEASE);   // no decision yet
     s->gate_arm_seq = 0;
     extra = true;
@@ -3234,13 +3242,14 @@ int pft_slab_ipc_export(pft_slab* s, void* handles)
   return 0;
 }
 
-static int ipc_staged_env()
+int pft_ipc_staged_env(void)
 {
   const char* e = getenv("PFT_IPC_STAGED");
   return e && atoi(e) == 1;
 }
 
-int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, long fs, int device)
+int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, long fs, int device,
+                          int peer_staged)
 {
   if (side < 0 || side > 1) return -2;
   SlabPeer& p = s->peer[side];
@@ -3253,7 +3262,7 @@ int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, lo
     for (int b = 0; b < PFT_BUF_COUNT; ++b) p.base[b] = s->buf0[b] + s->plane;
     p.sig = s->sig;
     p.rbuf = s->rbuf;
-    p.staged = ipc_staged_env();
+    p.staged = pft_ipc_staged_env();
     p.n3 = s->d.n3;
     p.fs = s->fs;
     p.opened = 0;
@@ -3280,9 +3289,11 @@ int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, lo
   p.remote = device != mine;
   // A neighbour on another GPU writes into our receive buffer (uncached) rather than our ghost
   // planes, and we copy it in after the flag wait: no L2 of ours can hold a stale line of what it
-  // wrote.  Both sides take the same decision (remote is symmetric; the env
-  // is the test hook that stages between processes on one GPU).
-  p.staged = p.remote || ipc_staged_env();
+  // wrote.  Both sides take the same decision: remote is symmetric, and the
+  // env (the test hook that stages between processes on one GPU) counts if either side set it --
+  // a sender putting into ghost planes that the receiver overwrites from its receive buffer, or
+  // the other way round, would corrupt the halo without any error.
+  p.staged = p.remote || pft_ipc_staged_env() || peer_staged;
   p.opened = 1;
   p.on = 1;
   return 0;

@@ -13,6 +13,7 @@ step caps of pft_solve_ex at every phase of the pipeline, calls that continue a 
 and RK_MPI_SA_solve's host boundary after a discarded gated step.
 """
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -116,3 +117,27 @@ def test_gated_host_boundary_calls(g100):
         out[gate] = recs
         sim.close()
     assert out[0] == out[1]
+
+
+def test_gated_discards_a_differing_decision(g100):
+    """the host's check of the device's decision: with every 5th accepted device decision's h off
+    by one bit (test hook PFT_GATE_FLIP), each such gated step is discarded and relaunched with the
+    host's h, and the trajectory is still the reference's, bit for bit"""
+    meta, A = g100
+    os.environ["PFT_GATE_FLIP"] = "5"
+    try:
+        sim = _sim(meta)
+    finally:
+        del os.environ["PFT_GATE_FLIP"]
+    misses = gated = 0
+    for i, T in enumerate(meta["traj_times"]):
+        rc = sim.solve(T)
+        ref = meta["traj_m0"][i]
+        assert (sim.t.hex(), sim.h.hex(), sim.system.steps, sim.system.steps_total, rc) == \
+            (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(), ref[2], ref[3], ref[4])
+        assert _sha(sim.interior()) == meta["traj_m0_sha256"][i]
+        st = sim.stats()
+        misses += st.gate_misses
+        gated += st.gated_steps
+    sim.close()
+    assert misses >= 10 and gated > 0, (misses, gated)

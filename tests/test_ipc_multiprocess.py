@@ -115,15 +115,16 @@ def test_400_processes_equal_one_slab(tmp_path, nranks):
     assert np.array_equal(np.concatenate([r["states"][0] for r in res], axis=1), x)
 
 
-@pytest.mark.parametrize("nranks,pair", [(2, 0), (3, 2)])
-def test_g20_processes_staged_receive_equal_reference(tmp_path, nranks, pair):
+@pytest.mark.parametrize("nranks,pair,staged_ranks", [(2, 0, (0, 1)), (3, 2, (0, 1, 2)), (3, 2, (1,))])
+def test_g20_processes_staged_receive_equal_reference(tmp_path, nranks, pair, staged_ranks):
     """the staged receive a neighbour on another GPU gets (here forced between processes on one
     GPU, PFT_IPC_STAGED=1): planes into the receiver's uncached receive buffer, copied into its
     ghost (and far ghost) planes after the flag wait -- golden g20 bit for bit, one launch per
-    stage and pair kernels (two-plane halo)"""
+    stage and pair kernels (two-plane halo).  staged_ranks (1,): only the middle rank asks for it;
+    its neighbours learn it at attach (IpcSlot.staged), so both ends of each link stage"""
     meta, A = O.load_case("g20")
     times = meta["traj_times"][:2]
-    env = {r: {"PFT_IPC_STAGED": "1"} for r in range(nranks)}
+    env = {r: {"PFT_IPC_STAGED": "1"} for r in staged_ranks}
     res = _run_ranks(tmp_path, nranks, rank_env=env, case="g20", times=times, tile=2, pair=pair)
     for r in res:
         assert int(r["path"]) == 1 and int(r["pairs"]) == (1 if pair else 0)
