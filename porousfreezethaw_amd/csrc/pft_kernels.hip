@@ -1219,6 +1219,9 @@ __device__ __forceinline__ dbl2 pair_in_B(const PairArgs& a, int q, const PairRa
 #ifndef PFT_PAIR_EO_MASK
 #define PFT_PAIR_EO_MASK 1
 #endif
+#ifndef PFT_PAIR_WIDE_Y
+#define PFT_PAIR_WIDE_Y 1
+#endif
 template <bool EO>
 struct PairLds;
 template <>
@@ -1266,6 +1269,17 @@ __device__ __forceinline__ void pair_rhs(const pft_consts& c, const double* L0, 
   constexpr bool FLUX = MODE != 10 && MODE != 11;
   using LD = PairLds<EO>;
   const double* L[3] = {L0, L1, L2};
+  // interleaved layout: the y neighbours of both cells as one 16-byte read per neighbouring pair
+  // (consecutive lanes, conflict-free) instead of two 8-byte reads at a 16-byte lane stride
+  constexpr bool WIDE = !EO && PFT_PAIR_WIDE_Y;
+  dbl2 ym2[3], yp2[3];
+  if constexpr (WIDE) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      ym2[q] = LD::ld(L[q], p - LWP);
+      yp2[q] = LD::ld(L[q], p + LWP);
+    }
+  }
   FaceT fx;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -1276,8 +1290,8 @@ __device__ __forceinline__ void pair_rhs(const pft_consts& c, const double* L0, 
       col[q].c = cen;
       col[q].xm = s == 0 ? LD::cell(L[q], p - 1, 1) : zc[q][0];   // odd cell of the pair to the left
       col[q].xp = s == 0 ? zc[q][1] : LD::cell(L[q], p + 1, 0);   // even cell of the pair to the right
-      col[q].ym = LD::cell(L[q], p - LWP, s);
-      col[q].yp = LD::cell(L[q], p + LWP, s);
+      col[q].ym = WIDE ? ym2[q][s] : LD::cell(L[q], p - LWP, s);
+      col[q].yp = WIDE ? yp2[q][s] : LD::cell(L[q], p + LWP, s);
       col[q].zm = zm[q][s];
       col[q].zp = zp[q][s];
     }
