@@ -1209,15 +1209,20 @@ __device__ __forceinline__ dbl2 pair_in_B(const PairArgs& a, int q, const PairRa
 
 // A pair from / to LDS at position slot p, with its cells exchanged when sw = 1 (two 8-byte
 // accesses at per-lane offsets).  Two layouts of a field plane (EO, a template parameter):
+//   EO = false (default): the cells of a position side by side (slot p: doubles 2p, 2p + 1); a
+//               cell on its own is an 8-byte access at a 16-byte lane stride (2-way bank
+//               conflicts), so pair_rhs reads the y neighbours of both cells as one 16-byte access
+//               per neighbouring pair (PFT_PAIR_WIDE_Y, conflict-free);
 //   EO = true : the even cells of the positions in one half, the odd cells PFT_PAIR_H doubles
-//               later (slot p: doubles p and PFT_PAIR_H + p) -- no bank conflicts;
-//   EO = false: the cells of a position side by side (slot p: doubles 2p, 2p + 1) -- 2-way bank
-//               conflicts (16-byte lane stride), but a mirrored lane's two accesses share a base.
-// Measured (A/B, one box, 400^3): pair 2+3 0.358 ms with EO against 0.362-0.365 interleaved;
-// pair 4+5 0.410-0.415 interleaved against 0.416-0.424 with EO (profiles/r04b_ab_pair_lds.txt):
-// the defaults below (PFT_PAIR_EO_MASK bit 0: pair 2+3, bit 1: pair 4+5).
+//               later (slot p: doubles p and PFT_PAIR_H + p) -- every access conflict-free, but
+//               no 16-byte accesses and more address registers.
+// Measured (A/B on one box each, 400^3; profiles/r04b_ab_small_grids_and_layouts.txt): pair 2+3
+// 0.362-0.365 ms interleaved, 0.357-0.359 EO, 0.352-0.356 interleaved with the wide y reads; pair
+// 4+5 0.416-0.424 EO, 0.410-0.415 interleaved, 0.409-0.411 with the wide y reads (reading the x
+// neighbours' pairs whole as well: no further change).  PFT_PAIR_EO_MASK bit 0: pair 2+3 EO, bit
+// 1: pair 4+5 EO.
 #ifndef PFT_PAIR_EO_MASK
-#define PFT_PAIR_EO_MASK 1
+#define PFT_PAIR_EO_MASK 0
 #endif
 #ifndef PFT_PAIR_WIDE_Y
 #define PFT_PAIR_WIDE_Y 1
