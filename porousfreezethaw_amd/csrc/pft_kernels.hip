@@ -680,6 +680,12 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 
 // LDS doubles per field and plane of merson_fused: (2 gwx + 4)(gty + 2) <= 680 (64 x 8 tiles)
 #define PFT_FUSED_LF 680
+#ifndef PFT_FUSED_WIDE_Y
+#define PFT_FUSED_WIDE_Y 1
+#endif
+#ifndef PFT_FUSED_NAT
+#define PFT_FUSED_NAT 1
+#endif
 
 // (non-temporal loads measured -25%, non-temporal stores +-0: plain accesses)
 __device__ __forceinline__ dbl2 ld2(const double* p) { return *reinterpret_cast<const dbl2*>(p); }
@@ -689,6 +695,12 @@ __device__ __forceinline__ void st2x(double* p, dbl2 v, int sw)
 {
   p[sw] = v.x;
   p[1 - sw] = v.y;
+}
+// merson_fused's LDS stores: natural order (one 16-byte store) under PFT_FUSED_NAT
+__device__ __forceinline__ void st2f(double* p, dbl2 v, int sw)
+{
+  if (PFT_FUSED_NAT) st2(p, v);
+  else st2x(p, v, sw);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -815,7 +827,12 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
   // Swapped pairs are stored as two 8-byte halves at exchanged offsets (per-thread constants),
   // not through per-store selects.
   const bool cswap = i0 == a.n1;
-  const int c0 = cswap ? 1 : 0, h0 = hswap ? 1 : 0;
+  // PFT_FUSED_NAT: every pair is stored in natural order (16-byte stores, no 8-byte halves at a
+  // 16-byte lane stride), and the thread next to a mirrored pair reads its other cell instead:
+  // (-2, -1) holds (v0, v1), cell -1 = its even cell; (n1, n1 + 1) holds (v[n1-2], v[n1-1]), cell
+  // n1 = its odd cell (xma / xpa: offsets of the x-neighbour reads)
+  const int c0 = PFT_FUSED_NAT ? 0 : (cswap ? 1 : 0), h0 = PFT_FUSED_NAT ? 0 : (hswap ? 1 : 0);
+  const int xma = PFT_FUSED_NAT && i0 - 2 < 0 ? 1 : 0, xpa = PFT_FUSED_NAT && i0 + 2 >= a.n1 ? 1 : 0;
 
   double m = 0.0;
   bool nf = false;
@@ -863,9 +880,9 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
       if constexpr (SUM2) s2c[q] = cop[q].k1;
       if (STAGE == 5) keep5<GLS>(q, cop[q], cx[q], ck1[q], ck4[q], cE[q]);
       zm[q] = wlo ? zc[q] : stage_in<STAGE, GLS>(a, q, bop[q]);
-      st2x(&lds[0][q][lo], zc[q], c0);
+      st2f(&lds[0][q][lo], zc[q], c0);
     }
-    if (hact) st2x(&lds[0][hf][hl], stage_in<STAGE, GLS>(a, hf, hop), h0);
+    if (hact) st2f(&lds[0][hf][hl], stage_in<STAGE, GLS>(a, hf, hop), h0);
     // the DEEP look-ahead after those loads are consumed, as before: the loop then starts with
     // only the look-ahead in flight (with it issued together with the rest, the compiler's wait
     // placement serialised the loop's own look-ahead: stage 1 at 400^3 0.149 -> 0.175 ms)
@@ -905,7 +922,7 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
     dbl2 hv = {0.0, 0.0};
     if (more) {
 #pragma unroll
-      for (int q = 0; q < 3; ++q) st2x(&lds[cur ^ 1][q][lo], zp[q], c0);
+      for (int q = 0; q < 3; ++q) st2f(&lds[cur ^ 1][q][lo], zp[q], c0);
       if (hact) {
         if constexpr (DEEP) {
           hv = stage_in<STAGE, GLS>(a, hf, ph);
@@ -933,6 +950,16 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
     }
     double du[2], dp[2];
     FaceT fx;                          // the x-face between the pair's two cells
+    // the y neighbours of both cells as one 16-byte LDS read per neighbouring pair (consecutive
+    // lanes: no bank conflicts, where two 8-byte reads at a 16-byte lane stride conflict 2-way)
+    dbl2 ym2[3], yp2[3];
+    if constexpr (PFT_FUSED_WIDE_Y) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        ym2[q] = ld2(&lds[cur][q][lo - LW]);
+        yp2[q] = ld2(&lds[cur][q][lo + LW]);
+      }
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       Col col[3];
@@ -942,10 +969,10 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
         const double cen = zc[q][s];
         col[q].c = cen;
         // x/y neighbours straight from LDS: the walls' mirror values are in the halo
-        col[q].xm = s == 0 ? L[lo - 1] : zc[q][0];
-        col[q].xp = s == 0 ? zc[q][1] : L[lo + 2];
-        col[q].ym = L[lo - LW + s];
-        col[q].yp = L[lo + LW + s];
+        col[q].xm = s == 0 ? L[lo - 1 - xma] : zc[q][0];
+        col[q].xp = s == 0 ? zc[q][1] : L[lo + 2 + xpa];
+        col[q].ym = PFT_FUSED_WIDE_Y ? ym2[q][s] : L[lo - LW + s];
+        col[q].yp = PFT_FUSED_WIDE_Y ? yp2[q][s] : L[lo + LW + s];
         col[q].zm = zm[q][s];
         col[q].zp = zp[q][s];
       }
@@ -956,7 +983,7 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
       rhs_cell_f<MODE>(c, col[0], col[1], col[2], un, fxm, fz[s], fx, fzp, du[s], dp[s]);
       fz[s] = fzp;
     }
-    if (more && hact) st2x(&lds[cur ^ 1][hf][hl], hv, h0);
+    if (more && hact) st2f(&lds[cur ^ 1][hf][hl], hv, h0);
     if (active) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
@@ -1251,12 +1278,9 @@ struct PairLds<true> {
 };
 template <>
 struct PairLds<false> {
-  __device__ static __forceinline__ dbl2 ld(const double* L, int p, int sw)
-  {
-    const double* q = L + 2 * p;
-    return dbl2{q[sw], q[1 - sw]};
-  }
-  __device__ static __forceinline__ void st(double* L, int p, dbl2 v, int sw) { st2x(L + 2 * p, v, sw); }
+  // (mirrored positions are stored in natural order in this layout: sw is always 0)
+  __device__ static __forceinline__ dbl2 ld(const double* L, int p, int) { return ld2(L + 2 * p); }
+  __device__ static __forceinline__ void st(double* L, int p, dbl2 v, int) { st2(L + 2 * p, v); }
   __device__ static __forceinline__ dbl2 ld(const double* L, int p) { return ld2(L + 2 * p); }
   __device__ static __forceinline__ void st(double* L, int p, dbl2 v) { st2(L + 2 * p, v); }
   __device__ static __forceinline__ double cell(const double* L, int p, int s) { return L[2 * p + s]; }
@@ -1268,7 +1292,7 @@ struct PairLds<false> {
 // (rhs_cell_f, bit-exact), as in merson_fused
 template <int MODE, int LWP, bool EO>
 __device__ __forceinline__ void pair_rhs(const pft_consts& c, const double* L0, const double* L1, const double* L2,
-                                         int p, const dbl2* zm, const dbl2* zc, const dbl2* zp,
+                                         int p, int xmc, int xpc, const dbl2* zm, const dbl2* zc, const dbl2* zp,
                                          const double* nz, FaceT* fz, double* du, double* dp)
 {
   constexpr bool FLUX = MODE != 10 && MODE != 11;
@@ -1293,8 +1317,10 @@ __device__ __forceinline__ void pair_rhs(const pft_consts& c, const double* L0, 
     for (int q = 0; q < 3; ++q) {
       const double cen = zc[q][s];
       col[q].c = cen;
-      col[q].xm = s == 0 ? LD::cell(L[q], p - 1, 1) : zc[q][0];   // odd cell of the pair to the left
-      col[q].xp = s == 0 ? zc[q][1] : LD::cell(L[q], p + 1, 0);   // even cell of the pair to the right
+      // the cell of the pair to the left / right next to this pair: its odd / even cell, or the
+      // other one where that slot holds a mirrored position in natural order (xmc / xpc)
+      col[q].xm = s == 0 ? LD::cell(L[q], p - 1, xmc) : zc[q][0];
+      col[q].xp = s == 0 ? zc[q][1] : LD::cell(L[q], p + 1, xpc);
       col[q].ym = WIDE ? ym2[q][s] : LD::cell(L[q], p - LWP, s);
       col[q].yp = WIDE ? yp2[q][s] : LD::cell(L[q], p + LWP, s);
       col[q].zm = zm[q][s];
@@ -1339,7 +1365,17 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   // acting pair (in the domain): a mirrored position holds its values (x halves exchanged)
   const int ai = pi < 0 ? 0 : (pi >= a.n1 ? a.n1 - 2 : pi);
   const int aj = pj < 0 ? 0 : (pj >= a.n2 ? a.n2 - 1 : pj);
+  // A position outside the domain in x holds the mirror image of its acting pair.  Interleaved
+  // layout: the slot stores the acting pair in natural order (16-byte stores and loads, no
+  // per-lane swap), and the neighbour reading it takes the other cell (mirrored pair (-2, -1) =
+  // (v1, v0) holds (v0, v1): cell -1 is its even cell; (n1, n1 + 1) holds (v[n1-2], v[n1-1]): cell
+  // n1 is its odd cell).  EO layout: the slot stores the swapped pair (sw).
   const int xsw = (pi < 0 || pi >= a.n1) ? 1 : 0;
+  const int sw = EO ? xsw : 0;
+  auto mir = [&](int col) -> bool { const int c0 = x0 - 2 + 2 * col; return c0 < 0 || c0 >= a.n1; };
+  const int pxa = (ai - x0 + 2) / 2;                          // the acting pair's column
+  const int xmcA = EO ? 1 : (mir(pxa - 1) ? 0 : 1), xpcA = EO ? 0 : (mir(pxa + 1) ? 1 : 0);
+  const int xmcB = EO ? 1 : (mir(px - 1) ? 0 : 1), xpcB = EO ? 0 : (mir(px + 1) ? 1 : 0);
   const unsigned apo = (unsigned)(aj * a.n1 + ai);
   // byte offset of the acting pair in plane m of a field, from the PairArgs pointers
   auto pbo = [&](int m) -> unsigned { return ((unsigned)(m + 2) * (unsigned)a.plane + apo) * 8u; };
@@ -1385,18 +1421,18 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         iam[q] = pair_in_A<SA, GLX>(a, q, t);
-        LD::st(lA[2][q], posA, iam[q], xsw);
+        LD::st(lA[2][q], posA, iam[q], sw);
       }
     }
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       ia0[q] = pair_in_A<SA, GLX>(a, q, R[0]);
-      LD::st(lA[0][q], posA, ia0[q], xsw);
+      LD::st(lA[0][q], posA, ia0[q], sw);
       if (mA0 == mfirst) {
         // bottom wall: plane -1 mirrors plane 0 (equation.c:164-174), also in the ring slot of
         // plane -1, so that the z-loop reads its z neighbours without selects
         iam[q] = ia0[q];
-        LD::st(lA[2][q], posA, ia0[q], xsw);
+        LD::st(lA[2][q], posA, ia0[q], sw);
       }
     }
 #pragma unroll
@@ -1421,7 +1457,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
       // placement lost track of them and stage A waited for the look-ahead it had just issued.
       if (mm + 1 <= mlast) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) LD::st(lA[sAp][q], posA, pair_in_A<SA, GLX>(A0, q, rn), xsw);
+        for (int q = 0; q < 3; ++q) LD::st(lA[sAp][q], posA, pair_in_A<SA, GLX>(A0, q, rn), sw);
       }
       if (mm + 2 <= mlast) pair_load<SA>(A0, pbo(mm + 2), rnn);          // look-ahead
     }
@@ -1449,20 +1485,20 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
         dbl2 zc[3], zm[3], zp[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          zc[q] = LD::ld(lA[sA][q], posA, xsw);
-          zm[q] = LD::ld(lA[sAm][q], posA, xsw);
-          zp[q] = LD::ld(lA[sAp][q], posA, xsw);
+          zc[q] = LD::ld(lA[sA][q], posA, sw);
+          zm[q] = LD::ld(lA[sAm][q], posA, sw);
+          zp[q] = LD::ld(lA[sAp][q], posA, sw);
         }
         double du[2], dp[2];
         const double* nz = A1.noise ? A1.noise + (long)mm * A1.plane + (long)apo : nullptr;
-        pair_rhs<MODE, LWP, EO>(C1, lA[sA][0], lA[sA][1], lA[sA][2], actA, zm, zc, zp, nz, fzA, du, dp);
+        pair_rhs<MODE, LWP, EO>(C1, lA[sA][0], lA[sA][1], lA[sA][2], actA, xmcA, xpcA, zm, zc, zp, nz, fzA, du, dp);
         ka[0] = dbl2{du[0], du[1]};
         ka[1] = dbl2{dp[0], dp[1]};
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
           const dbl2 ib = pair_in_B<SA, GLX>(A1, q, rc, q < 2 ? ka[q < 2 ? q : 0] : zero2);
-          LD::st(lB[sA][q], posB, ib, xsw);
-          if (mm == 0 && wlo) LD::st(lB[sAm][q], posB, ib, xsw);   // bottom wall: plane -1 mirrors plane 0
+          LD::st(lB[sA][q], posB, ib, sw);
+          if (mm == 0 && wlo) LD::st(lB[sAm][q], posB, ib, sw);   // bottom wall: plane -1 mirrors plane 0
         }
       }
     }
@@ -1506,7 +1542,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
         double du[2], dp[2];
         const unsigned e0 = pbo(kB);
         const double* nz = A2.noise ? A2.noise + (long)kB * A2.plane + (long)apo : nullptr;
-        pair_rhs<MODE, LWP, EO>(C2, lB[sB][0], lB[sB][1], lB[sB][2], lo, zm, zc, zp, nz, fzB, du, dp);
+        pair_rhs<MODE, LWP, EO>(C2, lB[sB][0], lB[sB][1], lB[sB][2], lo, xmcB, xpcB, zm, zc, zp, nz, fzB, du, dp);
         if (SA == 2) {
           stb(A2.out, e0, dbl2{du[0], du[1]});                   // K3 (hybrid2.c:412-429)
           stb(A2.out + A2.fs, e0, dbl2{dp[0], dp[1]});
