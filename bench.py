@@ -148,11 +148,11 @@ def main():
         # libpft's communicator (pft_comm.h).  torch never touches the GPU here.
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        comm = make_comm(L, a.transport, world, rank, dev, dist)
+        comm, a.transport = make_comm(L, a.transport, world, rank, dev, dist)
     else:
         L.pft_hip_set_device(dev)
         if a.self_exchange:
-            comm = make_comm(L, a.transport, 1, 0, dev, None)
+            comm, a.transport = make_comm(L, a.transport, 1, 0, dev, None)
             assert L.pft_comm_set_self_exchange(comm, 1) == 0
     L.pft_solver_set_option(P.PFT_OPT_DEVICE, dev)
     L.pft_solver_set_option(P.PFT_OPT_GATE, a.gate)
@@ -455,9 +455,13 @@ def parity_check(ranks, calls, a, base, dims, Ls, beads, final_time, dev):
             "mismatches": bad, "seconds": round(time.time() - t0, 1)}
 
 
-def make_comm(L, transport, world, rank, dev, dist):
-    """libpft communicator of this rank (pft_comm.h), bound to this thread.  The rendezvous data
-    (ipc: a shared-memory name, rccl: the unique id) goes through torch.distributed's gloo store."""
+def make_comm(L, transport, world, rank, dev, dist, fallback=True):
+    """libpft communicator of this rank (pft_comm.h), bound to this thread, and the transport it
+    uses.  The rendezvous data (ipc: a shared-memory name, rccl: the unique id) goes through
+    torch.distributed's gloo store.  If the RCCL communicator fails to initialise on any rank
+    (every rank learns it through gloo), all ranks fall back to the ipc transport -- across GPUs its
+    staged receive -- so that an N > 1 run still measures, and checks its parity, rather than
+    ending; the JSON line then names the transport that ran."""
     comm = C.c_void_p()
     if transport == "ipc":
         name = [f"/pft_bench_{os.getpid()}_{int(time.time() * 1e6) % 10**9}"]
@@ -473,10 +477,20 @@ def make_comm(L, transport, world, rank, dev, dist):
             dist.broadcast_object_list(obj, src=0)
             uid = (C.c_char * 128).from_buffer_copy(obj[0])
         rc = L.pft_comm_init_rccl(C.byref(comm), world, rank, uid, dev)
+        if dist is not None and fallback:
+            import torch
+            bad = torch.tensor([1 if rc else 0], dtype=torch.int64)
+            dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+            if int(bad.item()):
+                if rc == 0:
+                    L.pft_comm_destroy(comm)
+                print(f"rank {rank}: the RCCL communicator failed to initialise on a rank ({rc} here); "
+                      f"every rank falls back to the ipc transport", file=sys.stderr)
+                return make_comm(L, "ipc", world, rank, dev, dist, fallback=False)
     if rc:
         sys.exit(f"rank {rank}: pft_comm_init_{transport} failed ({rc})")
     L.pft_comm_set_current(comm)
-    return comm
+    return comm, transport
 
 
 def workload(grid_nodes, world, shape="cube", literal_cube=False, mode=0, domain=None):
