@@ -1254,6 +1254,9 @@ __device__ __forceinline__ dbl2 pair_in_B(const PairArgs& a, int q, const PairRa
 #ifndef PFT_PAIR_WIDE_Y
 #define PFT_PAIR_WIDE_Y 1
 #endif
+#ifndef PFT_PAIR_ZREG         // pair 2+3: stage A's own-position inputs from registers (A/B: 0)
+#define PFT_PAIR_ZREG 1
+#endif
 template <bool EO>
 struct PairLds;
 template <>
@@ -1407,6 +1410,12 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   // register rotation needs no copies.
   PairRaw R[3];
   dbl2 KA[3][2];        // stage A's K (u, p) of the last three planes, rotating with R
+  // PFT_PAIR_ZREG (pair 2+3, which has the registers: 218 VGPRs with it): stage A's inputs at
+  // this thread's own position, plane by ring slot, kept in registers beside their LDS copies --
+  // stage A reads its z neighbours and centre from here instead of from LDS (measured: pair 2+3
+  // 0.362 -> 0.354 ms, 200^3 +1.0%; profiles/r04b_ab_small_grids_and_layouts.txt ab4q)
+  constexpr bool ZREG = SA == 2 && PFT_PAIR_ZREG;
+  dbl2 IA[3][3];
   FaceT fzA[2], fzB[2];
 
   // prologue: stage A's input of planes mA0 - 1 (if any) and mA0 into the ring (slots 2 and 0);
@@ -1422,17 +1431,20 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
       for (int q = 0; q < 3; ++q) {
         iam[q] = pair_in_A<SA, GLX>(a, q, t);
         LD::st(lA[2][q], posA, iam[q], sw);
+        if (ZREG) IA[2][q] = iam[q];
       }
     }
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       ia0[q] = pair_in_A<SA, GLX>(a, q, R[0]);
       LD::st(lA[0][q], posA, ia0[q], sw);
+      if (ZREG) IA[0][q] = ia0[q];
       if (mA0 == mfirst) {
         // bottom wall: plane -1 mirrors plane 0 (equation.c:164-174), also in the ring slot of
         // plane -1, so that the z-loop reads its z neighbours without selects
         iam[q] = ia0[q];
         LD::st(lA[2][q], posA, ia0[q], sw);
+        if (ZREG) IA[2][q] = ia0[q];
       }
     }
 #pragma unroll
@@ -1457,7 +1469,11 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
       // placement lost track of them and stage A waited for the look-ahead it had just issued.
       if (mm + 1 <= mlast) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) LD::st(lA[sAp][q], posA, pair_in_A<SA, GLX>(A0, q, rn), sw);
+        for (int q = 0; q < 3; ++q) {
+          const dbl2 v = pair_in_A<SA, GLX>(A0, q, rn);
+          LD::st(lA[sAp][q], posA, v, sw);
+          if (ZREG) IA[sAp][q] = v;
+        }
       }
       if (mm + 2 <= mlast) pair_load<SA>(A0, pbo(mm + 2), rnn);          // look-ahead
     }
@@ -1481,13 +1497,18 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
 #pragma unroll
           for (int q = 1; q < 3; ++q) LD::st(lA[sAp][q], posA, LD::ld(lA[sA][q], posA));
           LD::st(lA[sAp][0], posA, dbl2{A1.T_topA, A1.T_topA});
+          if (ZREG) {
+            IA[sAp][1] = IA[sA][1];
+            IA[sAp][2] = IA[sA][2];
+            IA[sAp][0] = dbl2{A1.T_topA, A1.T_topA};
+          }
         }
         dbl2 zc[3], zm[3], zp[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          zc[q] = LD::ld(lA[sA][q], posA, sw);
-          zm[q] = LD::ld(lA[sAm][q], posA, sw);
-          zp[q] = LD::ld(lA[sAp][q], posA, sw);
+          zc[q] = ZREG ? IA[sA][q] : LD::ld(lA[sA][q], posA, sw);
+          zm[q] = ZREG ? IA[sAm][q] : LD::ld(lA[sAm][q], posA, sw);
+          zp[q] = ZREG ? IA[sAp][q] : LD::ld(lA[sAp][q], posA, sw);
         }
         double du[2], dp[2];
         const double* nz = A1.noise ? A1.noise + (long)mm * A1.plane + (long)apo : nullptr;
