@@ -1257,6 +1257,10 @@ __device__ __forceinline__ dbl2 pair_in_B(const PairArgs& a, int q, const PairRa
 #ifndef PFT_PAIR_ZREG         // pair 2+3: stage A's own-position inputs from registers (A/B: 0)
 #define PFT_PAIR_ZREG 1
 #endif
+#ifndef PFT_PAIR_OPL          // pair 4+5 (GLX): stage B's output operands kept in LDS (A/B: 0)
+#define PFT_PAIR_OPL 1
+#endif
+#define PFT_PAIR_OPN 384      // stage-B positions of a tile ((tx/2) ty, at most 380: pair_geometry_ok)
 template <bool EO>
 struct PairLds;
 template <>
@@ -1354,8 +1358,17 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
 #endif
   // (the interleaved layout's stage-B ring holds rows 1..ty+2 only: PFT_PAIR_HB slots, no padding
   // to the halves -- its LDS offsets, and with them the registers the kernel needs, as in round 3)
+  // PFT_PAIR_OPL (pair 4+5 with GLX, interleaved layout): stage B's gl input is x's gl, which
+  // lA already holds for the same plane -- lB keeps u and p only and stage B reads gl from lA
+  // (its z neighbour below from a register: lA's slot of that plane is overwritten by then).  The
+  // 22 KiB this frees, with the 22 KiB left over, hold the operands of stage B's outputs (x, K1,
+  // K3 of u and p at each stage-B position, 36 KiB): written when they arrive for stage A, read
+  // back one plane later by the same thread, instead of their second load from beyond L2.
+  constexpr bool OPL = SA == 4 && GLX && !EO && PFT_PAIR_OPL;
+  constexpr int NBQ = OPL ? 2 : 3;   // lB's fields
   __shared__ __attribute__((aligned(16))) double lA[3][3][2 * PFT_PAIR_H];
-  __shared__ __attribute__((aligned(16))) double lB[3][3][EO ? 2 * PFT_PAIR_H : 2 * PFT_PAIR_HB];
+  __shared__ __attribute__((aligned(16))) double lB[3][NBQ][EO ? 2 * PFT_PAIR_H : 2 * PFT_PAIR_HB];
+  __shared__ __attribute__((aligned(16))) dbl2 lO[OPL ? 6 : 1][OPL ? PFT_PAIR_OPN : 1];
 
   const int TX = a.tx, TY = a.ty, WP2 = TX / 2 + 2, NPOS = WP2 * (TY + 4);
   const int lin = xcd_remap(blockIdx.x, a.ntile * a.nchunk);
@@ -1388,6 +1401,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   const bool isA = py >= 1 && py <= TY + 2;
   const bool isB = (int)threadIdx.x < NPOS && px >= 1 && px <= TX / 2 && py >= 2 && py <= TY + 1 &&
                    pi < a.n1 && pj < a.n2;
+  const int ob = (py - 2) * (TX / 2) + px - 1;                // this stage-B position's slot in lO
 
   const int kb = a.k_begin + chunk * a.kz;
   const int ke = min(kb + a.kspan, a.k_end);
@@ -1416,6 +1430,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   // 0.362 -> 0.354 ms, 200^3 +1.0%; profiles/r04b_ab_small_grids_and_layouts.txt ab4q)
   constexpr bool ZREG = SA == 2 && PFT_PAIR_ZREG;
   dbl2 IA[3][3];
+  dbl2 glm = zero2;     // OPL: gl's input at this position, plane mm - 2 (stage B's z neighbour below)
   FaceT fzA[2], fzB[2];
 
   // prologue: stage A's input of planes mA0 - 1 (if any) and mA0 into the ring (slots 2 and 0);
@@ -1461,6 +1476,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
     {
       PFT_PAIR_BIND(A0, C0);
       (void)C0;
+      if (OPL) glm = LD::ld(lA[sAp][2], posA);                 // plane mm - 2, before mm + 1 replaces it
       // stage A's input of plane mm + 1 (own pair: read back by this thread in this iteration;
       // x/y neighbours: in the next one, behind the barrier), and the look-ahead load of plane
       // mm + 2.  Both unconditional -- beyond mlast the load re-reads plane mlast and the store
@@ -1516,7 +1532,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
         ka[0] = dbl2{du[0], du[1]};
         ka[1] = dbl2{dp[0], dp[1]};
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
+        for (int q = 0; q < NBQ; ++q) {
           const dbl2 ib = pair_in_B<SA, GLX>(A1, q, rc, q < 2 ? ka[q < 2 ? q : 0] : zero2);
           LD::st(lB[sA][q], posB, ib, sw);
           if (mm == 0 && wlo) LD::st(lB[sAm][q], posB, ib, sw);   // bottom wall: plane -1 mirrors plane 0
@@ -1537,22 +1553,49 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
       // an ablation gained ~1%)
       // (GLX: gl's x(t+h) is not stored, XN holds it: gl's x is not needed)
       // (unconditional, as the look-ahead: every lane's acting pair is in the domain)
-      if (SA == 4 && kB >= kb && isB) pair_load<SA, !GLX>(A2, pbo(kB), ro);
+      if (OPL) {
+        // plane kB's operands from lO, then plane mm's into the same slot (this thread's own; LDS
+        // accesses of a wave stay in order)
+        if (kB >= kb && isB) {
+          ro.x[0] = lO[0][ob];
+          ro.x[1] = lO[1][ob];
+          ro.k1[0] = lO[2][ob];
+          ro.k1[1] = lO[3][ob];
+          ro.k3[0] = lO[4][ob];
+          ro.k3[1] = lO[5][ob];
+        }
+        if (isB && mm >= kb && mm < ke) {
+          lO[0][ob] = rc.x[0];
+          lO[1][ob] = rc.x[1];
+          lO[2][ob] = rc.k1[0];
+          lO[3][ob] = rc.k1[1];
+          lO[4][ob] = rc.k3[0];
+          lO[5][ob] = rc.k3[1];
+        }
+      } else if (SA == 4 && kB >= kb && isB) {
+        pair_load<SA, !GLX>(A2, pbo(kB), ro);
+      }
       if (kB >= kb && isB) {
         constexpr int sB = (PH + 2) % 3, sBm = (PH + 1) % 3, sBp = PH;   // slots of planes kB, kB-1, kB+1
         const int lo = posB;
         if (kB == n3 - 1 && whi) {
           // top wall: the ghost values of plane n3 at this position (as in stage A above)
 #pragma unroll
-          for (int q = 1; q < 3; ++q) LD::st(lB[sBp][q], lo, LD::ld(lB[sB][q], lo));
+          // (OPL: gl's ghost is in lA's slot of plane n3, from stage A's top wall)
+          for (int q = 1; q < NBQ; ++q) LD::st(lB[sBp][q], lo, LD::ld(lB[sB][q], lo));
           LD::st(lB[sBp][0], lo, dbl2{A2.T_topB, A2.T_topB});
         }
         dbl2 zc[3], zm[3], zp[3];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
+        for (int q = 0; q < NBQ; ++q) {
           zc[q] = LD::ld(lB[sB][q], lo);
           zm[q] = LD::ld(lB[sBm][q], lo);
           zp[q] = LD::ld(lB[sBp][q], lo);
+        }
+        if (OPL) {
+          zc[2] = LD::ld(lA[sB][2], posA);
+          zm[2] = glm;
+          zp[2] = LD::ld(lA[sBp][2], posA);
         }
         if (kB == kb) {
           // the z-face below the chunk's first stage-B plane
@@ -1563,7 +1606,9 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
         double du[2], dp[2];
         const unsigned e0 = pbo(kB);
         const double* nz = A2.noise ? A2.noise + (long)kB * A2.plane + (long)apo : nullptr;
-        pair_rhs<MODE, LWP, EO>(C2, lB[sB][0], lB[sB][1], lB[sB][2], lo, xmcB, xpcB, zm, zc, zp, nz, fzB, du, dp);
+        // (OPL: gl's plane from lA, whose rows start one row earlier: slot lo + LWP there)
+        const double* lBgl = OPL ? &lA[sB][2][2 * LWP] : &lB[sB][NBQ - 1][0];
+        pair_rhs<MODE, LWP, EO>(C2, lB[sB][0], lB[sB][1], lBgl, lo, xmcB, xpcB, zm, zc, zp, nz, fzB, du, dp);
         if (SA == 2) {
           stb(A2.out, e0, dbl2{du[0], du[1]});                   // K3 (hybrid2.c:412-429)
           stb(A2.out + A2.fs, e0, dbl2{dp[0], dp[1]});
@@ -3101,7 +3146,8 @@ static bool pair_geometry_ok(int tx, int ty)
 {
   const int lwp = pair_lwp(tx);
   return tx >= 2 && tx % 2 == 0 && ty >= 1 && (tx / 2 + 2) * (ty + 4) <= PFT_PBLOCK && tx / 2 + 2 <= 22 &&
-         2 * PFT_PAIR_PADP + lwp * (ty + 4) <= PFT_PAIR_H && 2 * PFT_PAIR_PADP + lwp * (ty + 2) <= PFT_PAIR_HB;
+         2 * PFT_PAIR_PADP + lwp * (ty + 4) <= PFT_PAIR_H && 2 * PFT_PAIR_PADP + lwp * (ty + 2) <= PFT_PAIR_HB &&
+         (tx / 2) * ty <= PFT_PAIR_OPN;
 }
 
 // automatic tile: the fewest workgroups per plane (a workgroup-plane costs about the same whatever
