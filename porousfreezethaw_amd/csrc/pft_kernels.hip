@@ -1418,7 +1418,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   bool nf = false;
   // Operands in registers: those of plane mm (stage B's input), mm + 1 (landed: stage A's input)
   // and mm + 2 (in flight), rotating through R[0..2]; stage B's outputs (4+5) need plane mm - 1's
-  // again: re-loaded after stage A (keeping them would hold ~60 doubles per thread and spill).
+  // again: from lO (OPL), else re-loaded after stage A (in registers they would spill).
   // Plane p's LDS ring slot is (p - mA0) mod 3 and the loop is unrolled three times, so every ring
   // slot -- and with the fixed row pitch every LDS offset -- is a compile-time constant, and the
   // register rotation needs no copies.
@@ -1544,13 +1544,12 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
       if (SA == 4) __builtin_amdgcn_s_setprio(0);
       else if ((threadIdx.x >> 8) == 0) __builtin_amdgcn_s_setprio(0);
       else __builtin_amdgcn_s_setprio(2);
-      // operands of plane kB for stage B's outputs (4+5), loaded a second time, after stage A:
-      // fewer registers live during stage A (keeping them would need ~60 VGPRs more than the 255
-      // in use), and the latency hides behind stage B's stencil.  NOT an L2 hit: their first load
-      // was the look-ahead three planes earlier, and three planes of the ring's operands of the
-      // ~32 workgroups of an XCD (~5 MB) exceed its 4 MB L2 -- the Infinity Cache serves them
-      // (PMC: 1.78x the algorithmic bytes beyond L2; skipping the re-load in
-      // an ablation gained ~1%)
+      // operands of plane kB for stage B's outputs (4+5).  OPL: from lO.  Otherwise loaded a
+      // second time, after stage A (in registers they would need ~60 VGPRs more than the 255 in
+      // use), and NOT an L2 hit: their first load was the look-ahead three planes earlier, and
+      // three planes of the ring's operands of the ~32 workgroups of an XCD (~5 MB) exceed its
+      // 4 MB L2 -- the Infinity Cache serves them (PMC: 1.80x the algorithmic bytes beyond L2
+      // with the re-load, 1.11x with lO; pair 4+5 -1.5%: DESIGN.md section 5)
       // (GLX: gl's x(t+h) is not stored, XN holds it: gl's x is not needed)
       // (unconditional, as the look-ahead: every lane's acting pair is in the domain)
       if (OPL) {
