@@ -93,6 +93,45 @@ def test_pair_gl_static_and_noise(gl_static, noise, mode):
     _same(got, ref)
 
 
+@pytest.mark.parametrize("kz", [None, 2])
+@pytest.mark.parametrize("dims", [(66, 38, 21), (30, 30, 60)])
+def test_pair_gl_negative_zero(dims, kz):
+    """a -0.0 in gl turns gl_keep off (pft_slab_set_gl_keep): the pair kernels without GLX, whose
+    stage B keeps gl in its own ring and re-loads the operands of its outputs (no lO), against the
+    stage launches and the oracle, bit for bit and sign for sign"""
+    meta, _ = O.load_case("g20")
+    Pm, info = O.params_from_meta(meta)
+    n1, n2, n3 = dims
+    info = dict(info, n1=n1, n2=n2, n3=n3)
+    sim = P.Simulation(n1, n2, n3, (info["L1"], info["L2"], info["L3"]), 0, Pm, beads=O.beads(), tau=1.0,
+                       tau_min=info["tau_min"], delta=info["delta"], init_solver=False)
+    ic = sim.interior().copy()
+    sim.close()
+    ic[2, :, :5, :] = 0.0
+    ic[2, 3:9, :3, 2:11] = -0.0
+    assert np.signbit(ic[2]).sum() > 0
+    L = P.lib()
+    outs = []
+    for pair in (2, 0):
+        L.pft_solver_set_option(P.PFT_OPT_PAIR, pair)
+        try:
+            sim = P.Simulation(n1, n2, n3, (info["L1"], info["L2"], info["L3"]), 0, Pm, initial=ic, tau=1.0,
+                               tau_min=info["tau_min"], delta=info["delta"], tile=2, recompute=True, kz=kz)
+            assert sim.solve_ex(1e9, 10, 0) == 2
+            st = sim.stats()
+            outs.append((sim.t, sim.h, sim.system.steps, sim.system.steps_total, sim.interior(), st.pairs))
+            sim.close()
+        finally:
+            L.pft_solver_set_option(P.PFT_OPT_PAIR, 1)
+    got, ref = outs
+    assert got[5] == 1 and ref[5] == 0
+    assert got[:4] == ref[:4]
+    assert np.array_equal(got[4], ref[4]) and np.array_equal(np.signbit(got[4]), np.signbit(ref[4]))
+    res = O.solve(info, Pm, 0, ic, 0.0, 1.0, [1e9], max_steps_total=10)[0]
+    assert got[:4] == (res[0], res[1], res[2], res[3])
+    assert np.array_equal(got[4], res[5]) and np.array_equal(np.signbit(got[4][2]), np.signbit(res[5][2]))
+
+
 @pytest.mark.parametrize("dims", [(30, 30, 60), (100, 36, 40), (18, 12, 30)])
 def test_pair_matches_oracle(dims):
     got, used, ic, info, Pm = _run(dims, 0, True, 12)
