@@ -1260,6 +1260,9 @@ __device__ __forceinline__ dbl2 pair_in_B(const PairArgs& a, int q, const PairRa
 #ifndef PFT_PAIR_OPL          // pair 4+5 (GLX): stage B's output operands kept in LDS (A/B: 0)
 #define PFT_PAIR_OPL 1
 #endif
+#ifndef PFT_PAIR_GLB23        // pair 2+3 (GLX): stage B's gl from the stage-A ring / registers (A/B: 0)
+#define PFT_PAIR_GLB23 1
+#endif
 #define PFT_PAIR_OPN 384      // stage-B positions of a tile ((tx/2) ty, at most 380: pair_geometry_ok)
 template <bool EO>
 struct PairLds;
@@ -1364,8 +1367,11 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   // 22 KiB this frees, with the 22 KiB left over, hold the operands of stage B's outputs (x, K1,
   // K3 of u and p at each stage-B position, 36 KiB): written when they arrive for stage A, read
   // back one plane later by the same thread, instead of their second load from beyond L2.
-  constexpr bool OPL = SA == 4 && GLX && !EO && PFT_PAIR_OPL;
-  constexpr int NBQ = OPL ? 2 : 3;   // lB's fields
+  // (GLB: the same gl sharing in pair 2+3, whose ZREG registers hold stage A's gl inputs at the
+  // thread's own position: stage B's gl centre and z neighbours come from there)
+  constexpr bool GLB = GLX && !EO && (SA == 4 ? PFT_PAIR_OPL : PFT_PAIR_GLB23);
+  constexpr bool OPL = SA == 4 && GLB;
+  constexpr int NBQ = GLB ? 2 : 3;   // lB's fields
   __shared__ __attribute__((aligned(16))) double lA[3][3][2 * PFT_PAIR_H];
   __shared__ __attribute__((aligned(16))) double lB[3][NBQ][EO ? 2 * PFT_PAIR_H : 2 * PFT_PAIR_HB];
   __shared__ __attribute__((aligned(16))) dbl2 lO[OPL ? 6 : 1][OPL ? PFT_PAIR_OPN : 1];
@@ -1430,7 +1436,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   // 0.362 -> 0.354 ms, 200^3 +1.0%; profiles/r04b_ab_small_grids_and_layouts.txt ab4q)
   constexpr bool ZREG = SA == 2 && PFT_PAIR_ZREG;
   dbl2 IA[3][3];
-  dbl2 glm = zero2;     // OPL: gl's input at this position, plane mm - 2 (stage B's z neighbour below)
+  dbl2 glm = zero2;     // GLB: gl's input at this position, plane mm - 2 (stage B's z neighbour below)
   FaceT fzA[2], fzB[2];
 
   // prologue: stage A's input of planes mA0 - 1 (if any) and mA0 into the ring (slots 2 and 0);
@@ -1476,7 +1482,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
     {
       PFT_PAIR_BIND(A0, C0);
       (void)C0;
-      if (OPL) glm = LD::ld(lA[sAp][2], posA);                 // plane mm - 2, before mm + 1 replaces it
+      if (GLB) glm = ZREG ? IA[sAp][2] : LD::ld(lA[sAp][2], posA);   // plane mm - 2, before mm + 1 replaces it
       // stage A's input of plane mm + 1 (own pair: read back by this thread in this iteration;
       // x/y neighbours: in the next one, behind the barrier), and the look-ahead load of plane
       // mm + 2.  Both unconditional -- beyond mlast the load re-reads plane mlast and the store
@@ -1580,7 +1586,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
         if (kB == n3 - 1 && whi) {
           // top wall: the ghost values of plane n3 at this position (as in stage A above)
 #pragma unroll
-          // (OPL: gl's ghost is in lA's slot of plane n3, from stage A's top wall)
+          // (GLB: gl's ghost is in lA's slot of plane n3, from stage A's top wall)
           for (int q = 1; q < NBQ; ++q) LD::st(lB[sBp][q], lo, LD::ld(lB[sB][q], lo));
           LD::st(lB[sBp][0], lo, dbl2{A2.T_topB, A2.T_topB});
         }
@@ -1591,10 +1597,10 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
           zm[q] = LD::ld(lB[sBm][q], lo);
           zp[q] = LD::ld(lB[sBp][q], lo);
         }
-        if (OPL) {
-          zc[2] = LD::ld(lA[sB][2], posA);
+        if (GLB) {
+          zc[2] = ZREG ? IA[sB][2] : LD::ld(lA[sB][2], posA);
           zm[2] = glm;
-          zp[2] = LD::ld(lA[sBp][2], posA);
+          zp[2] = ZREG ? IA[sBp][2] : LD::ld(lA[sBp][2], posA);
         }
         if (kB == kb) {
           // the z-face below the chunk's first stage-B plane
@@ -1605,8 +1611,8 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
         double du[2], dp[2];
         const unsigned e0 = pbo(kB);
         const double* nz = A2.noise ? A2.noise + (long)kB * A2.plane + (long)apo : nullptr;
-        // (OPL: gl's plane from lA, whose rows start one row earlier: slot lo + LWP there)
-        const double* lBgl = OPL ? &lA[sB][2][2 * LWP] : &lB[sB][NBQ - 1][0];
+        // (GLB: gl's plane from lA, whose rows start one row earlier: slot lo + LWP there)
+        const double* lBgl = GLB ? &lA[sB][2][2 * LWP] : &lB[sB][NBQ - 1][0];
         pair_rhs<MODE, LWP, EO>(C2, lB[sB][0], lB[sB][1], lBgl, lo, xmcB, xpcB, zm, zc, zp, nz, fzB, du, dp);
         if (SA == 2) {
           stb(A2.out, e0, dbl2{du[0], du[1]});                   // K3 (hybrid2.c:412-429)
