@@ -476,6 +476,17 @@ def make_comm(L, transport, world, rank, dev, dist, fallback=True):
             obj = [bytes(uid)]
             dist.broadcast_object_list(obj, src=0)
             uid = (C.c_char * 128).from_buffer_copy(obj[0])
+            if fallback:
+                # ncclCommInitRank is collective: a rank that would fail before entering it (its
+                # device cannot be set) would leave the others inside it for good, so every rank's
+                # local precheck is agreed first, and a failure anywhere goes to ipc before RCCL
+                import torch
+                pre = torch.tensor([0 if L.pft_hip_set_device(dev) == 0 else 1], dtype=torch.int64)
+                dist.all_reduce(pre, op=dist.ReduceOp.MAX)
+                if int(pre.item()):
+                    print(f"rank {rank}: a rank cannot set its device for RCCL; every rank falls back to the "
+                          f"ipc transport", file=sys.stderr)
+                    return make_comm(L, "ipc", world, rank, dev, dist, fallback=False)
         rc = L.pft_comm_init_rccl(C.byref(comm), world, rank, uid, dev)
         if dist is not None and fallback:
             import torch
@@ -570,4 +581,15 @@ def cpu_baseline(sim, base, a):
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except SystemExit:
+        raise
+    except BaseException:   # noqa: BLE001
+        # a failed solve (a lost peer: the solver's bounded waits return PFT_SOLVE_DEVICE_ERROR)
+        # ends this rank at once with a non-zero status; its closed gloo sockets end the others'
+        # collectives instead of leaving them to time out
+        import traceback
+        traceback.print_exc()
+        sys.stderr.flush()
+        os._exit(1)

@@ -288,6 +288,15 @@ int pft_slab_halo_wait(pft_slab * s, unsigned long long seq);
    (RK_MPI_SA_solve: PFT_SOLVE_DEVICE_ERROR).  A neighbour on another GPU is staged (above). */
 #define PFT_ERR_IPC_TIMEOUT (-5002)
 int pft_slab_sync(pft_slab * s);
+/* A communicator whose work the compute stream waits on (RCCL) bounds the slab's host waits the
+   same way: while a watch is set, every host wait (pft_slab_sync, the error-norm fetch, up/download)
+   polls, and calls fn(ctx, expired) about every millisecond, expired = 1 once timeout_s has passed
+   since the wait began.  A nonzero return (the communicator saw an asynchronous error, or the
+   expiry, and aborted: PFT_ERR_COMM_ABORTED) ends the wait with that code, and the slab refuses
+   every later wait, exchange and error-norm fetch until it is destroyed.  fn = NULL removes it. */
+#define PFT_ERR_COMM_ABORTED (-5003)
+typedef int (*pft_slab_watch_fn)(void * ctx, int expired);
+int pft_slab_set_watch(pft_slab * s, pft_slab_watch_fn fn, void * ctx, double timeout_s);
 
 /* peer copy of one ghost plane between slabs on the same process (loopback transport) */
 int pft_memcpy_d2d_async(void * dst, const void * src, size_t bytes, void * stream);

@@ -217,6 +217,10 @@ class Simulation:
     def __init__(self, n1, n2, total_n3, L, calc_mode, params, nprocs=1, rank=0, beads=None,
                  initial=None, tau=1.0, tau_min=0.0, delta=1e-3, t0=0.0, gl_static=False, kz=None,
                  init_solver=True, tile=None, recompute=True, icond=None, device_ic=False):
+        if device_ic and (icond is not None or initial is not None or not init_solver):
+            # checked before any host IC work: the device IC overwrites X/XN and the host copy
+            raise ValueError("device_ic computes the default Params' IC on an initialised solver: "
+                             "it cannot be combined with initial=, icond= or init_solver=False")
         L1, L2, L3 = L
         self.lib = L_ = lib()
         self.grid = pft_grid()
@@ -281,7 +285,6 @@ class Simulation:
         if device_ic:
             # f1: the default Params' IC and the beads computed on the device (bit for bit the
             # host's); the host array receives a copy, so every later call works as after a host IC
-            assert icond is None and initial is None and self.initialised, "device_ic: default IC, solver initialised"
             rc = L_.pft_solver_ic_default_device(1 if beads is not None else 0)
             if rc:
                 raise RuntimeError(f"pft_solver_ic_default_device failed ({rc}): {L_.pft_hip_last_error()}")

@@ -82,6 +82,14 @@ struct pft_comm {
   unsigned long long dseq;   // device halo exchanges so far (identical on every rank)
   double timeout_s;
   void* bcast_pinned;        // rccl: pinned host staging of pft_comm_bcast
+  // rccl: every host wait on RCCL work is bounded (PFT_COMM_TIMEOUT, default 300 s) and watches
+  // ncclCommGetAsyncError; on expiry or an error the communicator is aborted (ncclCommAbort) and
+  // every later call refuses (PFT_ERR_COMM_ABORTED)
+  int aborted;
+  long halos;                        // exchanges started so far
+  long stall_after;                  // test hook PFT_COMM_STALL=n: the n-th exchange's comm stream
+  unsigned long long* stall_word;    // waits on this word (uncached device memory), released only
+  hipStream_t stall_stream;          // by the abort -- a peer that never arrives, on one GPU
 };
 
 static __thread pft_comm* g_current = nullptr;
@@ -132,6 +140,69 @@ static int ipc_round(pft_comm* c, const unsigned long long v[2], long long iv, c
   }
   *recs = R;
   return 0;
+}
+
+// ---- rccl watchdog -------------------------------------------------------------------------
+static double comm_timeout_env()
+{
+  const char* e = getenv("PFT_COMM_TIMEOUT");
+  return (e && atof(e) > 0.0) ? atof(e) : 300.0;
+}
+
+static int rccl_abort(pft_comm* c, const char* why)
+{
+  if (c->aborted) return PFT_ERR_COMM_ABORTED;
+  fprintf(stderr, "pft_comm(rccl): rank %d: %s: aborting the communicator\n", c->rank, why);
+  c->aborted = 1;
+  if (c->stall_word) {
+    // the test hook's stalled comm stream goes on first, so that nothing still waits on it while
+    // the abort frees the communicator's resources
+    static const unsigned long long go = ~0ULL >> 1;
+    (void)hipMemcpyAsync(c->stall_word, &go, 8, hipMemcpyHostToDevice, c->stall_stream);
+    (void)hipStreamSynchronize(c->stall_stream);
+  }
+  // the abort flag ends RCCL kernels waiting for a peer; the frees inside wait for the device
+  (void)ncclCommAbort(c->nccl);
+  c->nccl = nullptr;
+  (void)hipGetLastError();
+  return PFT_ERR_COMM_ABORTED;
+}
+
+// pft_slab_watch_fn of an RCCL communicator: its asynchronous error, or the expiry of a host wait
+static int rccl_watch(void* ctx, int expired)
+{
+  pft_comm* c = (pft_comm*)ctx;
+  if (c->aborted) return PFT_ERR_COMM_ABORTED;
+  ncclResult_t ae = ncclSuccess;
+  if (ncclCommGetAsyncError(c->nccl, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+    return rccl_abort(c, ncclGetErrorString(ae));
+  if (expired) return rccl_abort(c, "no progress within PFT_COMM_TIMEOUT");
+  return 0;
+}
+
+// the host waits for stream st, which carries RCCL work: bounded and watched as above
+static int rccl_stream_wait(pft_comm* c, hipStream_t st)
+{
+  double t0 = 0.0;
+  for (long it = 0;; ++it) {
+    const hipError_t q = hipStreamQuery(st);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) {
+      fprintf(stderr, "pft_comm: hipStreamQuery: %s\n", hipGetErrorString(q));
+      (void)hipGetLastError();
+      return -1000 - (int)q;
+    }
+    if (it < 20000) {
+      __builtin_ia32_pause();
+    } else {
+      sched_yield();
+      if ((it & 1023) == 0) {
+        if (t0 == 0.0) t0 = now_s();
+        const int rc = rccl_watch(c, now_s() - t0 > c->timeout_s);
+        if (rc) return rc;
+      }
+    }
+  }
 }
 
 #define NCCLCHK(x)                                                         \
@@ -192,6 +263,14 @@ int pft_comm_init_rccl(pft_comm** c, int nranks, int rank, const void* id_bytes,
   HCHK(hipEventCreateWithFlags(&m->ev_ready, hipEventDisableTiming));
   HCHK(hipEventCreateWithFlags(&m->ev_done, hipEventDisableTiming));
   HCHK(hipMalloc(&m->dscratch, 256));
+  m->timeout_s = comm_timeout_env();
+  const char* es = getenv("PFT_COMM_STALL");
+  m->stall_after = es ? atol(es) : 0;
+  if (m->stall_after > 0) {
+    HCHK(hipExtMallocWithFlags((void**)&m->stall_word, 64, hipDeviceMallocUncached));
+    HCHK(hipMemset(m->stall_word, 0, 64));
+    HCHK(hipStreamCreateWithFlags(&m->stall_stream, hipStreamNonBlocking));
+  }
   *c = m;
   return 0;
 }
@@ -306,10 +385,13 @@ int pft_comm_destroy(pft_comm* c)
   if (!c) return 0;
   if (g_current == c) g_current = nullptr;
   if (c->kind == KIND_RCCL) {
-    ncclCommDestroy(c->nccl);
+    if (c->slab) (void)pft_slab_set_watch(c->slab, nullptr, nullptr, 0.0);
+    if (!c->aborted) ncclCommDestroy(c->nccl);
     (void)hipEventDestroy(c->ev_ready);
     (void)hipEventDestroy(c->ev_done);
     (void)hipFree(c->dscratch);
+    if (c->stall_word) (void)hipFree(c->stall_word);
+    if (c->stall_stream) (void)hipStreamDestroy(c->stall_stream);
   }
   if (c->kind == KIND_IPC) {
     if (c->slab) pft_comm_attach(c, nullptr);
@@ -398,6 +480,11 @@ int pft_comm_attach(pft_comm* c, pft_slab* s)
 {
   if (!c) return -2;
   if (c->kind == KIND_IPC) return c->slab == s ? 0 : ipc_attach(c, s);
+  if (c->kind == KIND_RCCL && c->slab != s) {
+    // the slab's host waits (error norm, sync, up/download) wait on RCCL-fed streams: bounded
+    if (c->slab) (void)pft_slab_set_watch(c->slab, nullptr, nullptr, 0.0);
+    if (s) (void)pft_slab_set_watch(s, rccl_watch, c, c->timeout_s);
+  }
   c->slab = s;
   if (c->kind == KIND_LOOP) c->grp->slabs[c->rank] = s;
   return 0;
@@ -426,9 +513,12 @@ static int halo_start(pft_comm* c, int buf, int f0, int f1, bool deep = false)
     return rc ? rc : pft_slab_halo_wait(s, seq);
   }
   if (c->kind == KIND_RCCL) {
+    if (c->aborted) return PFT_ERR_COMM_ABORTED;
     hipStream_t cs = (hipStream_t)pft_slab_comm_stream(s);
     HCHK(hipEventRecord(c->ev_ready, st));
     HCHK(hipStreamWaitEvent(cs, c->ev_ready, 0));
+    if (++c->halos == c->stall_after)
+      HCHK(hipStreamWaitValue64(cs, c->stall_word, 1, hipStreamWaitValueGte, ~0ULL));
     NCCLCHK(ncclGroupStart());
     // deep: also the second planes into / from the far ghost planes; per peer the sends and the
     // peer's receives pair up in the same order (field by field: ghost plane, then far plane)
@@ -515,6 +605,7 @@ int pft_comm_allreduce_eps(pft_comm* c)
   hipStream_t st = (hipStream_t)pft_slab_stream(s);
   unsigned long long* d = (unsigned long long*)pft_slab_scratch(s);
   if (c->kind == KIND_RCCL) {
+    if (c->aborted) return PFT_ERR_COMM_ABORTED;
     // max of non-negative doubles == max of their bit patterns; flag: max of 0/1
     NCCLCHK(ncclAllReduce(d, d, 2, ncclUint64, ncclMax, c->nccl, st));
     return 0;
@@ -546,6 +637,7 @@ int pft_comm_eps_publish(pft_comm* c)
   if (c->kind == KIND_RCCL) {
     // the max over ranks and the publication run on the communication stream, so the compute
     // stream goes on with the speculative stage 1 while RCCL reduces
+    if (c->aborted) return PFT_ERR_COMM_ABORTED;
     hipStream_t st = (hipStream_t)pft_slab_stream(s), cs = (hipStream_t)pft_slab_comm_stream(s);
     unsigned long long* d = (unsigned long long*)pft_slab_scratch(s);
     HCHK(hipEventRecord(c->ev_ready, st));
@@ -594,13 +686,15 @@ int pft_comm_bcast(pft_comm* c, void* data, int bytes, int root)
     // on the communication stream through pinned host memory: the host waits for that stream
     // only -- not for the compute stream's speculative stage 1 (the comm stream holds at most the
     // boundary planes' exchange of it)
+    if (c->aborted) return PFT_ERR_COMM_ABORTED;
     hipStream_t st = c->slab ? (hipStream_t)pft_slab_comm_stream(c->slab) : 0;
     if (!c->bcast_pinned) HCHK(hipHostMalloc(&c->bcast_pinned, 256, hipHostMallocDefault));
     memcpy(c->bcast_pinned, data, bytes);
     HCHK(hipMemcpyAsync(c->dscratch, c->bcast_pinned, bytes, hipMemcpyHostToDevice, st));
     NCCLCHK(ncclBroadcast(c->dscratch, c->dscratch, bytes, ncclUint8, root, c->nccl, st));
     HCHK(hipMemcpyAsync(c->bcast_pinned, c->dscratch, bytes, hipMemcpyDeviceToHost, st));
-    HCHK(hipStreamSynchronize(st));
+    const int rc = rccl_stream_wait(c, st);
+    if (rc) return rc;
     memcpy(data, c->bcast_pinned, bytes);
     return 0;
   }
@@ -625,12 +719,12 @@ int pft_comm_allreduce_max_i64(pft_comm* c, long long* v)
     return 0;
   }
   if (c->kind == KIND_RCCL) {
+    if (c->aborted) return PFT_ERR_COMM_ABORTED;
     hipStream_t st = c->slab ? (hipStream_t)pft_slab_stream(c->slab) : 0;
     HCHK(hipMemcpyAsync(c->dscratch, v, 8, hipMemcpyHostToDevice, st));
     NCCLCHK(ncclAllReduce(c->dscratch, c->dscratch, 1, ncclInt64, ncclMax, c->nccl, st));
     HCHK(hipMemcpyAsync(v, c->dscratch, 8, hipMemcpyDeviceToHost, st));
-    HCHK(hipStreamSynchronize(st));
-    return 0;
+    return rccl_stream_wait(c, st);
   }
   c->grp->ivals[c->rank] = *v;
   loop_barrier(c);

@@ -680,28 +680,10 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 
 // LDS doubles per field and plane of merson_fused: (2 gwx + 4)(gty + 2) <= 680 (64 x 8 tiles)
 #define PFT_FUSED_LF 680
-#ifndef PFT_FUSED_WIDE_Y
-#define PFT_FUSED_WIDE_Y 1
-#endif
-#ifndef PFT_FUSED_NAT
-#define PFT_FUSED_NAT 1
-#endif
 
 // (non-temporal loads measured -25%, non-temporal stores +-0: plain accesses)
 __device__ __forceinline__ dbl2 ld2(const double* p) { return *reinterpret_cast<const dbl2*>(p); }
 __device__ __forceinline__ void st2(double* p, dbl2 v) { *reinterpret_cast<dbl2*>(p) = v; }
-// store a pair with its halves exchanged when sw = 1 (two 8-byte stores at per-thread offsets)
-__device__ __forceinline__ void st2x(double* p, dbl2 v, int sw)
-{
-  p[sw] = v.x;
-  p[1 - sw] = v.y;
-}
-// merson_fused's LDS stores: natural order (one 16-byte store) under PFT_FUSED_NAT
-__device__ __forceinline__ void st2f(double* p, dbl2 v, int sw)
-{
-  if (PFT_FUSED_NAT) st2(p, v);
-  else st2x(p, v, sw);
-}
 
 // ------------------------------------------------------------------------------------------
 // the recompute kernel (default): an LDS tile, and no stage-input ("aux") array exists.
@@ -818,21 +800,18 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
   // Walls in LDS: a halo pair outside the domain holds the mirror image the reference's ghost
   // fill puts there (equation.c:137-174: ghost -1-m = interior m), so the stencil reads its x/y
   // neighbours without selects.  Pair (-2,-1) = (v1, v0): pair (0,1) swapped; pair (n1, n1+1) =
-  // (v[n1-1], v[n1-2]): pair (n1-2, n1-1) swapped; rows -1 / n2 = rows 0 / n2-1.
-  const bool hswap = hi < 0 || hi >= a.n1;
+  // (v[n1-1], v[n1-2]): pair (n1-2, n1-1) swapped (held in natural order, below); rows -1 / n2 =
+  // rows 0 / n2-1.
   const long hp = (long)(hj < 0 ? 0 : (hj >= a.n2 ? a.n2 - 1 : hj)) * a.n1 +
                   (hi < 0 ? 0 : (hi >= a.n1 ? a.n1 - 2 : hi));
   const int hl = hr * LW + 2 * hcp;
-  // an inactive pair just right of the domain (partial tile) is the mirror of the last pair.
-  // Swapped pairs are stored as two 8-byte halves at exchanged offsets (per-thread constants),
-  // not through per-store selects.
-  const bool cswap = i0 == a.n1;
-  // PFT_FUSED_NAT: every pair is stored in natural order (16-byte stores, no 8-byte halves at a
-  // 16-byte lane stride), and the thread next to a mirrored pair reads its other cell instead:
-  // (-2, -1) holds (v0, v1), cell -1 = its even cell; (n1, n1 + 1) holds (v[n1-2], v[n1-1]), cell
-  // n1 = its odd cell (xma / xpa: offsets of the x-neighbour reads)
-  const int c0 = PFT_FUSED_NAT ? 0 : (cswap ? 1 : 0), h0 = PFT_FUSED_NAT ? 0 : (hswap ? 1 : 0);
-  const int xma = PFT_FUSED_NAT && i0 - 2 < 0 ? 1 : 0, xpa = PFT_FUSED_NAT && i0 + 2 >= a.n1 ? 1 : 0;
+  // An inactive pair just right of the domain (partial tile) is the mirror of the last pair.  Every
+  // pair, mirrored ones included, is stored in natural order (16-byte stores), and the thread next
+  // to a mirrored pair reads its other cell instead: (-2, -1) holds (v0, v1), cell -1 = its even
+  // cell; (n1, n1 + 1) holds (v[n1-2], v[n1-1]), cell n1 = its odd cell (xma / xpa: offsets of the
+  // x-neighbour reads).  (Round 3 stored mirrored pairs as two 8-byte halves at exchanged offsets:
+  // 2-way LDS bank conflicts)
+  const int xma = i0 - 2 < 0 ? 1 : 0, xpa = i0 + 2 >= a.n1 ? 1 : 0;
 
   double m = 0.0;
   bool nf = false;
@@ -880,9 +859,9 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
       if constexpr (SUM2) s2c[q] = cop[q].k1;
       if (STAGE == 5) keep5<GLS>(q, cop[q], cx[q], ck1[q], ck4[q], cE[q]);
       zm[q] = wlo ? zc[q] : stage_in<STAGE, GLS>(a, q, bop[q]);
-      st2f(&lds[0][q][lo], zc[q], c0);
+      st2(&lds[0][q][lo], zc[q]);
     }
-    if (hact) st2f(&lds[0][hf][hl], stage_in<STAGE, GLS>(a, hf, hop), h0);
+    if (hact) st2(&lds[0][hf][hl], stage_in<STAGE, GLS>(a, hf, hop));
     // the DEEP look-ahead after those loads are consumed, as before: the loop then starts with
     // only the look-ahead in flight (with it issued together with the rest, the compiler's wait
     // placement serialised the loop's own look-ahead: stage 1 at 400^3 0.149 -> 0.175 ms)
@@ -922,7 +901,7 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
     dbl2 hv = {0.0, 0.0};
     if (more) {
 #pragma unroll
-      for (int q = 0; q < 3; ++q) st2f(&lds[cur ^ 1][q][lo], zp[q], c0);
+      for (int q = 0; q < 3; ++q) st2(&lds[cur ^ 1][q][lo], zp[q]);
       if (hact) {
         if constexpr (DEEP) {
           hv = stage_in<STAGE, GLS>(a, hf, ph);
@@ -953,12 +932,10 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
     // the y neighbours of both cells as one 16-byte LDS read per neighbouring pair (consecutive
     // lanes: no bank conflicts, where two 8-byte reads at a 16-byte lane stride conflict 2-way)
     dbl2 ym2[3], yp2[3];
-    if constexpr (PFT_FUSED_WIDE_Y) {
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        ym2[q] = ld2(&lds[cur][q][lo - LW]);
-        yp2[q] = ld2(&lds[cur][q][lo + LW]);
-      }
+    for (int q = 0; q < 3; ++q) {
+      ym2[q] = ld2(&lds[cur][q][lo - LW]);
+      yp2[q] = ld2(&lds[cur][q][lo + LW]);
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -971,8 +948,8 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
         // x/y neighbours straight from LDS: the walls' mirror values are in the halo
         col[q].xm = s == 0 ? L[lo - 1 - xma] : zc[q][0];
         col[q].xp = s == 0 ? zc[q][1] : L[lo + 2 + xpa];
-        col[q].ym = PFT_FUSED_WIDE_Y ? ym2[q][s] : L[lo - LW + s];
-        col[q].yp = PFT_FUSED_WIDE_Y ? yp2[q][s] : L[lo + LW + s];
+        col[q].ym = ym2[q][s];
+        col[q].yp = yp2[q][s];
         col[q].zm = zm[q][s];
         col[q].zp = zp[q][s];
       }
@@ -983,7 +960,7 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
       rhs_cell_f<MODE>(c, col[0], col[1], col[2], un, fxm, fz[s], fx, fzp, du[s], dp[s]);
       fz[s] = fzp;
     }
-    if (more && hact) st2f(&lds[cur ^ 1][hf][hl], hv, h0);
+    if (more && hact) st2(&lds[cur ^ 1][hf][hl], hv);
     if (active) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
@@ -1234,63 +1211,17 @@ __device__ __forceinline__ dbl2 pair_in_B(const PairArgs& a, int q, const PairRa
   return v;
 }
 
-// A pair from / to LDS at position slot p, with its cells exchanged when sw = 1 (two 8-byte
-// accesses at per-lane offsets).  Two layouts of a field plane (EO, a template parameter):
-//   EO = false (default): the cells of a position side by side (slot p: doubles 2p, 2p + 1); a
-//               cell on its own is an 8-byte access at a 16-byte lane stride (2-way bank
-//               conflicts), so pair_rhs reads the y neighbours of both cells as one 16-byte access
-//               per neighbouring pair (PFT_PAIR_WIDE_Y, conflict-free);
-//   EO = true : the even cells of the positions in one half, the odd cells PFT_PAIR_H doubles
-//               later (slot p: doubles p and PFT_PAIR_H + p) -- every access conflict-free, but
-//               no 16-byte accesses and more address registers.
-// Measured (A/B on one box each, 400^3; profiles/r04b_ab_small_grids_and_layouts.txt): pair 2+3
-// 0.362-0.365 ms interleaved, 0.357-0.359 EO, 0.352-0.356 interleaved with the wide y reads; pair
-// 4+5 0.416-0.424 EO, 0.410-0.415 interleaved, 0.409-0.411 with the wide y reads (reading the x
-// neighbours' pairs whole as well: no further change).  PFT_PAIR_EO_MASK bit 0: pair 2+3 EO, bit
-// 1: pair 4+5 EO.
-#ifndef PFT_PAIR_EO_MASK
-#define PFT_PAIR_EO_MASK 0
-#endif
-#ifndef PFT_PAIR_WIDE_Y
-#define PFT_PAIR_WIDE_Y 1
-#endif
-#ifndef PFT_PAIR_ZREG         // pair 2+3: stage A's own-position inputs from registers (A/B: 0)
-#define PFT_PAIR_ZREG 1
-#endif
-#ifndef PFT_PAIR_OPL          // pair 4+5 (GLX): stage B's output operands kept in LDS (A/B: 0)
-#define PFT_PAIR_OPL 1
-#endif
-#ifndef PFT_PAIR_GLB23        // pair 2+3 (GLX): stage B's gl from the stage-A ring / registers (A/B: 0)
-#define PFT_PAIR_GLB23 1
-#endif
+// A field plane of a ring holds the positions' cell pairs side by side (slot p: doubles 2p, 2p + 1),
+// mirrored positions in natural order (the neighbour reading one takes its other cell).  A cell read
+// on its own is an 8-byte access at a 16-byte lane stride (2-way bank conflicts), so pair_rhs reads
+// the y neighbours of both cells as one 16-byte access per neighbouring pair (consecutive lanes,
+// conflict-free).  Measured against it and removed (A/B on one box each, 400^3;
+// profiles/r04b_ab_small_grids_and_layouts.txt): the even and odd cells in two
+// halves (every access conflict-free, no 16-byte accesses, more address registers): pair 2+3
+// 0.357-0.359 ms against 0.352-0.356, pair 4+5 0.416-0.424 against 0.409-0.411 (a spill); the y
+// neighbours as two 8-byte reads: pair 2+3 0.362-0.365, pair 4+5 0.410-0.415.
 #define PFT_PAIR_OPN 384      // stage-B positions of a tile ((tx/2) ty, at most 380: pair_geometry_ok)
-template <bool EO>
-struct PairLds;
-template <>
-struct PairLds<true> {
-  static constexpr int H = PFT_PAIR_H;
-  __device__ static __forceinline__ dbl2 ld(const double* L, int p, int sw)
-  {
-    return dbl2{L[sw * H + p], L[(1 - sw) * H + p]};
-  }
-  __device__ static __forceinline__ void st(double* L, int p, dbl2 v, int sw)
-  {
-    L[sw * H + p] = v.x;
-    L[(1 - sw) * H + p] = v.y;
-  }
-  __device__ static __forceinline__ dbl2 ld(const double* L, int p) { return dbl2{L[p], L[H + p]}; }
-  __device__ static __forceinline__ void st(double* L, int p, dbl2 v)
-  {
-    L[p] = v.x;
-    L[H + p] = v.y;
-  }
-  __device__ static __forceinline__ double cell(const double* L, int p, int s) { return L[s * H + p]; }   // cell s of slot p
-};
-template <>
-struct PairLds<false> {
-  // (mirrored positions are stored in natural order in this layout: sw is always 0)
-  __device__ static __forceinline__ dbl2 ld(const double* L, int p, int) { return ld2(L + 2 * p); }
-  __device__ static __forceinline__ void st(double* L, int p, dbl2 v, int) { st2(L + 2 * p, v); }
+struct PairLds {
   __device__ static __forceinline__ dbl2 ld(const double* L, int p) { return ld2(L + 2 * p); }
   __device__ static __forceinline__ void st(double* L, int p, dbl2 v) { st2(L + 2 * p, v); }
   __device__ static __forceinline__ double cell(const double* L, int p, int s) { return L[2 * p + s]; }
@@ -1300,24 +1231,21 @@ struct PairLds<false> {
 // neighbours from the LDS field planes L[q] around slot p (even / odd halves, row pitch LWP); the
 // x-face between the pair's cells is evaluated once and the z-face below is carried in fz
 // (rhs_cell_f, bit-exact), as in merson_fused
-template <int MODE, int LWP, bool EO>
+template <int MODE, int LWP>
 __device__ __forceinline__ void pair_rhs(const pft_consts& c, const double* L0, const double* L1, const double* L2,
                                          int p, int xmc, int xpc, const dbl2* zm, const dbl2* zc, const dbl2* zp,
                                          const double* nz, FaceT* fz, double* du, double* dp)
 {
   constexpr bool FLUX = MODE != 10 && MODE != 11;
-  using LD = PairLds<EO>;
+  using LD = PairLds;
   const double* L[3] = {L0, L1, L2};
-  // interleaved layout: the y neighbours of both cells as one 16-byte read per neighbouring pair
-  // (consecutive lanes, conflict-free) instead of two 8-byte reads at a 16-byte lane stride
-  constexpr bool WIDE = !EO && PFT_PAIR_WIDE_Y;
+  // the y neighbours of both cells as one 16-byte read per neighbouring pair (consecutive lanes,
+  // conflict-free) instead of two 8-byte reads at a 16-byte lane stride
   dbl2 ym2[3], yp2[3];
-  if constexpr (WIDE) {
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      ym2[q] = LD::ld(L[q], p - LWP);
-      yp2[q] = LD::ld(L[q], p + LWP);
-    }
+  for (int q = 0; q < 3; ++q) {
+    ym2[q] = LD::ld(L[q], p - LWP);
+    yp2[q] = LD::ld(L[q], p + LWP);
   }
   FaceT fx;
 #pragma unroll
@@ -1331,8 +1259,8 @@ __device__ __forceinline__ void pair_rhs(const pft_consts& c, const double* L0, 
       // other one where that slot holds a mirrored position in natural order (xmc / xpc)
       col[q].xm = s == 0 ? LD::cell(L[q], p - 1, xmc) : zc[q][0];
       col[q].xp = s == 0 ? zc[q][1] : LD::cell(L[q], p + 1, xpc);
-      col[q].ym = WIDE ? ym2[q][s] : LD::cell(L[q], p - LWP, s);
-      col[q].yp = WIDE ? yp2[q][s] : LD::cell(L[q], p + LWP, s);
+      col[q].ym = ym2[q][s];
+      col[q].yp = yp2[q][s];
       col[q].zm = zm[q][s];
       col[q].zp = zp[q][s];
     }
@@ -1348,32 +1276,37 @@ __device__ __forceinline__ void pair_rhs(const pft_consts& c, const double* L0, 
 template <int N>
 using pft_ic = std::integral_constant<int, N>;
 
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Warray-bounds"
 template <int SA, int MODE, bool GLX, int LWP>
 __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2))) void merson_pair(PairArgs a,
                                                                                                    pft_consts c)
 {
   constexpr bool FLUX = MODE != 10 && MODE != 11;
   constexpr dbl2 zero2 = {0.0, 0.0};
-  constexpr bool EO = (PFT_PAIR_EO_MASK >> (SA == 2 ? 0 : 1)) & 1;
-  using LD = PairLds<EO>;
+  using LD = PairLds;
 #if defined(__HIP_DEVICE_COMPILE__)
   const pft_kptr kbase = (pft_kptr)__builtin_amdgcn_kernarg_segment_ptr();
 #endif
-  // (the interleaved layout's stage-B ring holds rows 1..ty+2 only: PFT_PAIR_HB slots, no padding
-  // to the halves -- its LDS offsets, and with them the registers the kernel needs, as in round 3)
-  // PFT_PAIR_OPL (pair 4+5 with GLX, interleaved layout): stage B's gl input is x's gl, which
+  // (the stage-B ring holds rows 1..ty+2 only: PFT_PAIR_HB slots)
+  // OPL (pair 4+5 with GLX): stage B's gl input is x's gl, which
   // lA already holds for the same plane -- lB keeps u and p only and stage B reads gl from lA
   // (its z neighbour below from a register: lA's slot of that plane is overwritten by then).  The
   // 22 KiB this frees, with the 22 KiB left over, hold the operands of stage B's outputs (x, K1,
   // K3 of u and p at each stage-B position, 36 KiB): written when they arrive for stage A, read
-  // back one plane later by the same thread, instead of their second load from beyond L2.
+  // back one plane later by the same thread, instead of their second load from beyond L2 (the
+  // re-load: pair 4+5 1.5% slower, 1.80x the algorithmic bytes beyond L2 against 1.11x).
   // (GLB: the same gl sharing in pair 2+3, whose ZREG registers hold stage A's gl inputs at the
-  // thread's own position: stage B's gl centre and z neighbours come from there)
-  constexpr bool GLB = GLX && !EO && (SA == 4 ? PFT_PAIR_OPL : PFT_PAIR_GLB23);
+  // thread's own position: stage B's gl centre and z neighbours come from there; without it pair
+  // 2+3 took 0.341-0.344 against 0.337-0.340 ms)
+  constexpr bool GLB = GLX;
   constexpr bool OPL = SA == 4 && GLB;
   constexpr int NBQ = GLB ? 2 : 3;   // lB's fields
   __shared__ __attribute__((aligned(16))) double lA[3][3][2 * PFT_PAIR_H];
-  __shared__ __attribute__((aligned(16))) double lB[3][NBQ][EO ? 2 * PFT_PAIR_H : 2 * PFT_PAIR_HB];
+  __shared__ __attribute__((aligned(16))) double lB[3][NBQ][2 * PFT_PAIR_HB];
+  // (without OPL a 1 x 1 placeholder: its accesses below sit in a branch that is constant-false
+  // there, which -Warray-bounds flags per instantiation; an if constexpr would drop the placeholder
+  // and shift the LDS layout of every other kernel)
   __shared__ __attribute__((aligned(16))) dbl2 lO[OPL ? 6 : 1][OPL ? PFT_PAIR_OPN : 1];
 
   const int TX = a.tx, TY = a.ty, WP2 = TX / 2 + 2, NPOS = WP2 * (TY + 4);
@@ -1387,17 +1320,14 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   // acting pair (in the domain): a mirrored position holds its values (x halves exchanged)
   const int ai = pi < 0 ? 0 : (pi >= a.n1 ? a.n1 - 2 : pi);
   const int aj = pj < 0 ? 0 : (pj >= a.n2 ? a.n2 - 1 : pj);
-  // A position outside the domain in x holds the mirror image of its acting pair.  Interleaved
-  // layout: the slot stores the acting pair in natural order (16-byte stores and loads, no
-  // per-lane swap), and the neighbour reading it takes the other cell (mirrored pair (-2, -1) =
-  // (v1, v0) holds (v0, v1): cell -1 is its even cell; (n1, n1 + 1) holds (v[n1-2], v[n1-1]): cell
-  // n1 is its odd cell).  EO layout: the slot stores the swapped pair (sw).
-  const int xsw = (pi < 0 || pi >= a.n1) ? 1 : 0;
-  const int sw = EO ? xsw : 0;
+  // A position outside the domain in x holds the mirror image of its acting pair: the slot stores
+  // the acting pair in natural order (16-byte stores and loads, no per-lane swap), and the
+  // neighbour reading it takes the other cell (mirrored pair (-2, -1) = (v1, v0) holds (v0, v1):
+  // cell -1 is its even cell; (n1, n1 + 1) holds (v[n1-2], v[n1-1]): cell n1 is its odd cell).
   auto mir = [&](int col) -> bool { const int c0 = x0 - 2 + 2 * col; return c0 < 0 || c0 >= a.n1; };
   const int pxa = (ai - x0 + 2) / 2;                          // the acting pair's column
-  const int xmcA = EO ? 1 : (mir(pxa - 1) ? 0 : 1), xpcA = EO ? 0 : (mir(pxa + 1) ? 1 : 0);
-  const int xmcB = EO ? 1 : (mir(px - 1) ? 0 : 1), xpcB = EO ? 0 : (mir(px + 1) ? 1 : 0);
+  const int xmcA = mir(pxa - 1) ? 0 : 1, xpcA = mir(pxa + 1) ? 1 : 0;
+  const int xmcB = mir(px - 1) ? 0 : 1, xpcB = mir(px + 1) ? 1 : 0;
   const unsigned apo = (unsigned)(aj * a.n1 + ai);
   // byte offset of the acting pair in plane m of a field, from the PairArgs pointers
   auto pbo = [&](int m) -> unsigned { return ((unsigned)(m + 2) * (unsigned)a.plane + apo) * 8u; };
@@ -1430,11 +1360,12 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   // register rotation needs no copies.
   PairRaw R[3];
   dbl2 KA[3][2];        // stage A's K (u, p) of the last three planes, rotating with R
-  // PFT_PAIR_ZREG (pair 2+3, which has the registers: 218 VGPRs with it): stage A's inputs at
-  // this thread's own position, plane by ring slot, kept in registers beside their LDS copies --
-  // stage A reads its z neighbours and centre from here instead of from LDS (measured: pair 2+3
-  // 0.362 -> 0.354 ms, 200^3 +1.0%; profiles/r04b_ab_small_grids_and_layouts.txt ab4q)
-  constexpr bool ZREG = SA == 2 && PFT_PAIR_ZREG;
+  // ZREG (pair 2+3, which has the registers: 218 VGPRs with it): stage A's inputs at this
+  // thread's own position, plane by ring slot, kept in registers beside their LDS copies -- stage
+  // A reads its z neighbours and centre from here instead of from LDS (measured: pair 2+3 0.362 ->
+  // 0.354 ms, 200^3 +1.0%; profiles/r04b_ab_small_grids_and_layouts.txt ab4q).  Pair 4+5 has no
+  // registers for it (256 VGPRs in use).
+  constexpr bool ZREG = SA == 2;
   dbl2 IA[3][3];
   dbl2 glm = zero2;     // GLB: gl's input at this position, plane mm - 2 (stage B's z neighbour below)
   FaceT fzA[2], fzB[2];
@@ -1451,20 +1382,20 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         iam[q] = pair_in_A<SA, GLX>(a, q, t);
-        LD::st(lA[2][q], posA, iam[q], sw);
+        LD::st(lA[2][q], posA, iam[q]);
         if (ZREG) IA[2][q] = iam[q];
       }
     }
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       ia0[q] = pair_in_A<SA, GLX>(a, q, R[0]);
-      LD::st(lA[0][q], posA, ia0[q], sw);
+      LD::st(lA[0][q], posA, ia0[q]);
       if (ZREG) IA[0][q] = ia0[q];
       if (mA0 == mfirst) {
         // bottom wall: plane -1 mirrors plane 0 (equation.c:164-174), also in the ring slot of
         // plane -1, so that the z-loop reads its z neighbours without selects
         iam[q] = ia0[q];
-        LD::st(lA[2][q], posA, ia0[q], sw);
+        LD::st(lA[2][q], posA, ia0[q]);
         if (ZREG) IA[2][q] = ia0[q];
       }
     }
@@ -1493,7 +1424,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
           const dbl2 v = pair_in_A<SA, GLX>(A0, q, rn);
-          LD::st(lA[sAp][q], posA, v, sw);
+          LD::st(lA[sAp][q], posA, v);
           if (ZREG) IA[sAp][q] = v;
         }
       }
@@ -1528,20 +1459,20 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
         dbl2 zc[3], zm[3], zp[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          zc[q] = ZREG ? IA[sA][q] : LD::ld(lA[sA][q], posA, sw);
-          zm[q] = ZREG ? IA[sAm][q] : LD::ld(lA[sAm][q], posA, sw);
-          zp[q] = ZREG ? IA[sAp][q] : LD::ld(lA[sAp][q], posA, sw);
+          zc[q] = ZREG ? IA[sA][q] : LD::ld(lA[sA][q], posA);
+          zm[q] = ZREG ? IA[sAm][q] : LD::ld(lA[sAm][q], posA);
+          zp[q] = ZREG ? IA[sAp][q] : LD::ld(lA[sAp][q], posA);
         }
         double du[2], dp[2];
         const double* nz = A1.noise ? A1.noise + (long)mm * A1.plane + (long)apo : nullptr;
-        pair_rhs<MODE, LWP, EO>(C1, lA[sA][0], lA[sA][1], lA[sA][2], actA, xmcA, xpcA, zm, zc, zp, nz, fzA, du, dp);
+        pair_rhs<MODE, LWP>(C1, lA[sA][0], lA[sA][1], lA[sA][2], actA, xmcA, xpcA, zm, zc, zp, nz, fzA, du, dp);
         ka[0] = dbl2{du[0], du[1]};
         ka[1] = dbl2{dp[0], dp[1]};
 #pragma unroll
         for (int q = 0; q < NBQ; ++q) {
           const dbl2 ib = pair_in_B<SA, GLX>(A1, q, rc, q < 2 ? ka[q < 2 ? q : 0] : zero2);
-          LD::st(lB[sA][q], posB, ib, sw);
-          if (mm == 0 && wlo) LD::st(lB[sAm][q], posB, ib, sw);   // bottom wall: plane -1 mirrors plane 0
+          LD::st(lB[sA][q], posB, ib);
+          if (mm == 0 && wlo) LD::st(lB[sAm][q], posB, ib);   // bottom wall: plane -1 mirrors plane 0
         }
       }
     }
@@ -1613,7 +1544,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
         const double* nz = A2.noise ? A2.noise + (long)kB * A2.plane + (long)apo : nullptr;
         // (GLB: gl's plane from lA, whose rows start one row earlier: slot lo + LWP there)
         const double* lBgl = GLB ? &lA[sB][2][2 * LWP] : &lB[sB][NBQ - 1][0];
-        pair_rhs<MODE, LWP, EO>(C2, lB[sB][0], lB[sB][1], lBgl, lo, xmcB, xpcB, zm, zc, zp, nz, fzB, du, dp);
+        pair_rhs<MODE, LWP>(C2, lB[sB][0], lB[sB][1], lBgl, lo, xmcB, xpcB, zm, zc, zp, nz, fzB, du, dp);
         if (SA == 2) {
           stb(A2.out, e0, dbl2{du[0], du[1]});                   // K3 (hybrid2.c:412-429)
           stb(A2.out + A2.fs, e0, dbl2{dp[0], dp[1]});
@@ -1682,6 +1613,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
     }
   }
 }
+#pragma clang diagnostic pop
 
 // ------------------------------------------------------------------------------------------
 // f1: the default Params' initial condition and the glass beads on the device (pft_slab_ic_default)
@@ -1975,8 +1907,9 @@ struct pft_slab {
   int ipc_poisoned;              // an ipc wait timed out: the flag words were forced past every
                                  // sequence number, so no later halo wait would block -- every halo
                                  // exchange, wait and sync refuses (PFT_ERR_IPC_TIMEOUT) until
-                                 // pft_slab_ipc_close resets the flags (a detach / re-attach)
-  double* staging;       // host padded layout on the device (for upload/download)
+                                 // pft_slab_ipc_close resets the flags (a detach / re-attach);
+                                 // 2: the watched communicator aborted (PFT_ERR_COMM_ABORTED, for good)
+  double* staging;      // host padded layout on the device (for upload/download)
   long S;                // host padded block (one field)
   unsigned long long* scratch;  // [0] eps bits, [1] nonfinite flag
   unsigned long long* host_scratch;  // pinned
@@ -2042,6 +1975,9 @@ struct pft_slab {
   long pair_ntile;
   double timeout_s;      // bound on a host wait for the compute stream while ipc peers are on
                          // (env PFT_IPC_TIMEOUT, default 300 s; slab_wait)
+  pft_slab_watch_fn watch;   // communicator watchdog (RCCL: async error / expiry -> abort)
+  void* watch_ctx;
+  double watch_timeout_s;
   // per-stage timing: a ring of begin/end event pairs, so that kernels still running when the
   // host collects (the speculative stage 1) are picked up by a later collect
   hipEvent_t tev[6][PFT_TRING][2];
@@ -2064,8 +2000,28 @@ static double wall_s()
 // PFT_ERR_IPC_TIMEOUT, which RK_MPI_SA_solve reports as PFT_SOLVE_DEVICE_ERROR.
 static int slab_poisoned(pft_slab* s, const char* what)
 {
+  if (s->ipc_poisoned == 2) {
+    snprintf(g_err, sizeof(g_err), "%s: the slab's communicator was aborted (PFT_COMM_TIMEOUT or an asynchronous error)", what);
+    return PFT_ERR_COMM_ABORTED;
+  }
   snprintf(g_err, sizeof(g_err), "%s: an earlier ipc halo wait timed out; detach and re-attach the slab", what);
   return PFT_ERR_IPC_TIMEOUT;
+}
+
+// the communicator watchdog (pft_slab_set_watch), called about every millisecond of a host wait;
+// t0: when the wait began (0: not yet taken).  Nonzero: the communicator aborted -- the slab
+// refuses from now on (its streams drained inside the abort, or will never: no later wait trusts them)
+static int slab_watch(pft_slab* s, double* t0, const char* what)
+{
+  if (*t0 == 0.0) *t0 = wall_s();
+  const int expired = wall_s() - *t0 > s->watch_timeout_s;
+  const int rc = s->watch(s->watch_ctx, expired);
+  if (!rc) return 0;
+  s->ipc_poisoned = 2;
+  snprintf(g_err, sizeof(g_err), "%s: the communicator aborted (%s)", what,
+           expired ? "no progress within PFT_COMM_TIMEOUT" : "asynchronous error");
+  fprintf(stderr, "libpft: %s\n", g_err);
+  return rc;
 }
 
 static int slab_timed_out(pft_slab* s, const char* what)
@@ -2087,16 +2043,18 @@ static int slab_timed_out(pft_slab* s, const char* what)
 static int slab_wait(pft_slab* s, hipEvent_t ev, const char* what)
 {
   if (s->ipc_poisoned) {
-    // the released flags let the stream drain: wait for it, then refuse
-    (void)hipStreamSynchronize(s->stream);
+    // ipc: the released flags let the stream drain: wait for it, then refuse.  An aborted
+    // communicator: refuse at once (nothing guarantees the stream drains)
+    if (s->ipc_poisoned == 1) (void)hipStreamSynchronize(s->stream);
     (void)hipGetLastError();
     return slab_poisoned(s, what);
   }
-  if (!s->peer[0].on && !s->peer[1].on) {
+  if (!s->peer[0].on && !s->peer[1].on && !s->watch) {
     HIPCHK(ev ? hipEventSynchronize(ev) : hipStreamSynchronize(s->stream));
     return 0;
   }
   const double t0 = wall_s();
+  double tw = 0.0;
   for (long it = 0;; ++it) {
     const hipError_t q = ev ? hipEventQuery(ev) : hipStreamQuery(s->stream);
     if (q == hipSuccess) return 0;
@@ -2105,7 +2063,14 @@ static int slab_wait(pft_slab* s, hipEvent_t ev, const char* what)
       __builtin_ia32_pause();
     } else {
       sched_yield();
-      if ((it & 1023) == 0 && wall_s() - t0 > s->timeout_s) return slab_timed_out(s, what);
+      if ((it & 1023) == 0) {
+        if (s->watch) {
+          const int rc = slab_watch(s, &tw, what);
+          if (rc) return rc;
+        } else if (wall_s() - t0 > s->timeout_s) {
+          return slab_timed_out(s, what);
+        }
+      }
     }
   }
 }
@@ -2113,6 +2078,15 @@ static int slab_wait(pft_slab* s, hipEvent_t ev, const char* what)
 extern "C" {
 
 int pft_slab_sync(pft_slab* s) { return s ? slab_wait(s, nullptr, "pft_slab_sync") : -2; }
+
+int pft_slab_set_watch(pft_slab* s, pft_slab_watch_fn fn, void* ctx, double timeout_s)
+{
+  if (!s || (fn && !(timeout_s > 0.0))) return -2;
+  s->watch = fn;
+  s->watch_ctx = fn ? ctx : nullptr;
+  s->watch_timeout_s = timeout_s;
+  return 0;
+}
 
 const char* pft_hip_last_error(void) { return g_err; }
 
@@ -2918,7 +2892,10 @@ int pft_slab_eps_fetch(pft_slab* s, double* eps, int* nonfinite)
         if (q != hipSuccess && q != hipErrorNotReady) return fail(q, "hipStreamQuery (error norm poll)");
         if (q == hipSuccess && __atomic_load_n(&w[1], __ATOMIC_ACQUIRE) == PFT_PUB_SENTINEL)
           return fail(hipErrorUnknown, "error norm never published");
-        if (s->peer[0].on || s->peer[1].on) {
+        if (s->watch) {
+          const int rc = slab_watch(s, &t0, "error norm poll");
+          if (rc) return rc;
+        } else if (s->peer[0].on || s->peer[1].on) {
           if (t0 == 0.0) t0 = wall_s();
           else if (wall_s() - t0 > s->timeout_s) return slab_timed_out(s, "error norm poll");
         }
@@ -3428,7 +3405,7 @@ int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, lo
 
 int pft_slab_ipc_close(pft_slab* s)
 {
-  if (s->ipc_poisoned) {
+  if (s->ipc_poisoned == 1) {
     // the flags were forced past every sequence number: back to 0 for the next attach (the compute
     // stream has drained, slab_wait)
     (void)hipStreamSynchronize(s->stream);

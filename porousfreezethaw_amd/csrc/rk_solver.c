@@ -590,7 +590,7 @@ static int run_fused(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcast
 					if(system->Service_Callback(final_time, system)) command |= RKA_CMD_BREAK;
 					R.in_callback = 0;
 				}
-				if(nprocs > 1 && B->any_cb) pft_comm_bcast(c, &command, sizeof(int), R.master);   /* :690 */
+				if(nprocs > 1 && B->any_cb && (rc = pft_comm_bcast(c, &command, sizeof(int), R.master))) return rc;   /* :690 */
 				if(command & RKA_CMD_FINISHED) break;                            /* :695 */
 				if(command & RKA_CMD_BREAK) {                                    /* :697-705 */
 					system->t = t;
@@ -694,19 +694,31 @@ int pft_solver_ic_default_device(int with_beads)
 	pft_comm * c = comm();
 	pft_ic_tables tb;
 	double * store = NULL;
-	int * istore = NULL, unclean = 0, rc;
+	int * istore = NULL, unclean = 0, rc, ret = 0;
 	long long u;
+	/* a rank that fails locally still takes part in the agreement below, so that no other rank is
+	   left inside a collective: every rank returns the same (most negative) code */
+	const long long FAILED = 1LL << 40;
 	if(R.max_n == 0) return -3;
-	if((rc = ensure_slab())) { R.last_status = rc; return PFT_SOLVE_DEVICE_ERROR; }
-	if((rc = pft_model_ic_tables(&tb, with_beads, &store, &istore))) return rc;
-	rc = pft_slab_ic_default(R.slab, &tb, &unclean);
+	if((rc = ensure_slab())) { R.last_status = rc; ret = PFT_SOLVE_DEVICE_ERROR; }
+	else if((rc = pft_model_ic_tables(&tb, with_beads, &store, &istore))) ret = rc;
+	else {
+		rc = pft_slab_ic_default(R.slab, &tb, &unclean);
+		if(rc) { R.last_status = rc; ret = PFT_SOLVE_DEVICE_ERROR; }
+	}
 	free(store);
 	free(istore);
-	if(rc) { R.last_status = rc; return PFT_SOLVE_DEVICE_ERROR; }
-	u = unclean;
+	u = ret ? FAILED - ret : unclean;
+	if(pft_comm_size(c) > 1 && (rc = pft_comm_allreduce_max_i64(c, &u))) {
+		R.last_status = rc;
+		return PFT_SOLVE_DEVICE_ERROR;
+	}
+	if(u >= FAILED) return (int)(FAILED - u);
 	if(pft_comm_size(c) > 1) {
-		if((rc = pft_comm_allreduce_max_i64(c, &u)) || (rc = pft_comm_halo(c, PFT_BUF_X, 0, 3)) ||
-		   (rc = pft_comm_halo(c, PFT_BUF_XN, 0, 3))) { R.last_status = rc; return PFT_SOLVE_DEVICE_ERROR; }
+		if((rc = pft_comm_halo(c, PFT_BUF_X, 0, 3)) || (rc = pft_comm_halo(c, PFT_BUF_XN, 0, 3))) {
+			R.last_status = rc;
+			return PFT_SOLVE_DEVICE_ERROR;
+		}
 	}
 	pft_slab_set_gl_keep(R.slab, !u);
 	R.device_valid = 1;
@@ -837,9 +849,9 @@ static int run_staged(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcas
 		                          R.d_k4, R.d_k5, R.d_aux, R.d_eps, NULL))) return rc;          /* :507-524 */
 		if((rc = pft_flat_d2h((double*)bits, R.d_eps, 2, NULL)) || (rc = pft_stream_sync(NULL))) return rc;
 		if(nprocs > 1) {
-			pft_comm_allreduce_max_i64(c, &bits[0]);                                            /* :572 */
+			if((rc = pft_comm_allreduce_max_i64(c, &bits[0]))) return rc;                      /* :572 */
 			bits[1] &= 0xffffffffLL;
-			pft_comm_allreduce_max_i64(c, &bits[1]);
+			if((rc = pft_comm_allreduce_max_i64(c, &bits[1]))) return rc;
 		}
 		memcpy(&eps, &bits[0], sizeof(double));
 		system->steps_total++;
@@ -880,7 +892,7 @@ static int run_staged(RK_MPI_S_SOLUTION * system, RK_RightHandSide f, solve_bcas
 					system->h = h;
 					if(system->Service_Callback(final_time, system)) command |= RKA_CMD_BREAK;
 				}
-				if(nprocs > 1 && B->any_cb) pft_comm_bcast(c, &command, sizeof(int), R.master);
+				if(nprocs > 1 && B->any_cb && (rc = pft_comm_bcast(c, &command, sizeof(int), R.master))) return rc;
 				if(command & RKA_CMD_FINISHED) break;
 				if(command & RKA_CMD_BREAK) { system->t = t; system->h = new_h; ret = 1; break; }
 				if(system->DDLBF_Rearrange != NULL) {                                              /* :726-729 */
@@ -914,7 +926,7 @@ int pft_solve_ex(FLOAT final_time, RK_MPI_S_SOLUTION * system, long max_steps_to
 {
 	pft_comm * c = comm();
 	const int rank = pft_comm_rank(c);
-	int error_code = 0, command = 0;
+	int error_code = 0, command = 0, crc;
 	long long neg;
 	RK_RightHandSide f = NULL;
 	solve_bcast B;
@@ -929,7 +941,9 @@ int pft_solve_ex(FLOAT final_time, RK_MPI_S_SOLUTION * system, long max_steps_to
 	if(system->x == NULL || system->meta_f == NULL) error_code = -2;            /* :284 */
 	if(rank == R.master && system->delta <= 0) error_code = -2;                 /* :286 */
 	neg = -error_code;                                                          /* :294 Allreduce(MIN) */
-	pft_comm_allreduce_max_i64(c, &neg);
+	/* a failed collective (a lost peer, an aborted communicator) is a device error on every rank
+	   that sees it; the bounded waits inside make sure each one returns */
+	if((crc = pft_comm_allreduce_max_i64(c, &neg))) { R.last_status = crc; return PFT_SOLVE_DEVICE_ERROR; }
 	if(error_code) return error_code;                                           /* :295 */
 	if(neg > 0) return -6;                                                      /* :299 */
 
@@ -946,8 +960,12 @@ int pft_solve_ex(FLOAT final_time, RK_MPI_S_SOLUTION * system, long max_steps_to
 		}
 	}
 	if(pft_comm_size(c) > 1) {                                                  /* :328-336 */
-		pft_comm_bcast(c, &B, sizeof(B), R.master);
-		{ long long cmd = command; pft_comm_allreduce_max_i64(c, &cmd); command = (int)cmd; }
+		long long cmd = command;
+		if((crc = pft_comm_bcast(c, &B, sizeof(B), R.master)) || (crc = pft_comm_allreduce_max_i64(c, &cmd))) {
+			R.last_status = crc;
+			return PFT_SOLVE_DEVICE_ERROR;
+		}
+		command = (int)cmd;
 	}
 	R.stats.nprocs = pft_comm_size(c);
 	R.stats.rank = rank;
