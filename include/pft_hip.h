@@ -154,6 +154,10 @@ typedef struct {
 	double s, R, reach2;                  /* 0.5/xi_gl, ball_radius, the host's cull distance^2 */
 } pft_ic_tables;
 int pft_slab_ic_default(pft_slab * s, const pft_ic_tables * t, int * gl_unclean);
+/* the beads of t over the gl already in X and XN (u, p kept; t's default-IC terms unused); with
+   nbeads = 0 only the gl scan for *gl_unclean */
+int pft_slab_ic_beads(pft_slab * s, const pft_ic_tables * t, int * gl_unclean);
+/* (f1 for any icond formula: pft_slab_ic_program, declared in pft_frontend.h) */
 
 /* error norm of the last stage 5: reset before the step, fetch after (blocks on the stream) */
 int pft_slab_eps_reset(pft_slab * s);

@@ -39,6 +39,14 @@ int pft_solver_download(RK_MPI_S_SOLUTION * system);
    Collective when the communicator has several ranks.  0, -3 (no RK_MPI_SA_init), -1 (beads
    requested but none set) or PFT_SOLVE_DEVICE_ERROR. */
 int pft_solver_ic_default_device(int with_beads);
+/* f1 for any icond formulas (intertrack.c:1831-2012): nprog compiled programs in the multi-pass
+   order (frontend.py icond_programs), program p for field qs[p] with lens[p] entries, concatenated
+   in ops/args (pft_frontend.h), then with with_beads the glass beads, all on the device into the
+   solver's state -- bit for bit pft_ic_eval + PrecalculateData on the host.  Returns 1 without
+   touching the device when a program is not device-exact (pft_ic_compile; every rank decides
+   alike: evaluate on the host), else as pft_solver_ic_default_device; -2 a bad program. */
+int pft_solver_ic_formulas_device(int nprog, const int * qs, const int * lens, const int * ops,
+                                  const double * args, int with_beads);
 
 /* RK_MPI_SA_solve / pft_solve_ex return value added to the reference's codes
    (RK_MPI_SAsolver.h:384-392): a HIP or RCCL failure (out of device memory, a device fault, a

@@ -131,6 +131,8 @@ def lib():
             getattr(L, name).restype = C.c_void_p
         L.pft_hip_device_count.argtypes = [ip]
         L.pft_hip_set_device.argtypes = [C.c_int]
+        L.pft_ic_device_ok.argtypes = [C.POINTER(pft_grid), C.c_int, ip, dp]
+        L.pft_solver_ic_formulas_device.argtypes = [C.c_int, ip, ip, ip, dp, C.c_int]
         L.pft_hip_last_error.restype = C.c_char_p
         L.pft_comm_get_unique_id.argtypes = [C.c_void_p]
         L.pft_comm_init_rccl.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_void_p, C.c_int]
@@ -217,10 +219,10 @@ class Simulation:
     def __init__(self, n1, n2, total_n3, L, calc_mode, params, nprocs=1, rank=0, beads=None,
                  initial=None, tau=1.0, tau_min=0.0, delta=1e-3, t0=0.0, gl_static=False, kz=None,
                  init_solver=True, tile=None, recompute=True, icond=None, device_ic=False):
-        if device_ic and (icond is not None or initial is not None or not init_solver):
+        if device_ic and (initial is not None or not init_solver):
             # checked before any host IC work: the device IC overwrites X/XN and the host copy
-            raise ValueError("device_ic computes the default Params' IC on an initialised solver: "
-                             "it cannot be combined with initial=, icond= or init_solver=False")
+            raise ValueError("device_ic computes the IC (the default Params', or icond=) on an initialised "
+                             "solver: it cannot be combined with initial= or init_solver=False")
         L1, L2, L3 = L
         self.lib = L_ = lib()
         self.grid = pft_grid()
@@ -234,7 +236,23 @@ class Simulation:
         self.N = (g.n3 + 4, g.n2 + 4, g.n1 + 4)
         self.S = int(np.prod(self.N))
         self.x = np.zeros(3 * self.S)
-        if icond is not None:
+        # where the IC is computed: "device" (f1: the default IC, or icond programs that compile for
+        # the device, pft_ic_compile), else "host"
+        self.ic_where = "host"
+        if device_ic and icond is not None:
+            ok = []
+            for q, prog in icond:
+                ops = np.array([o for o, _ in prog], dtype=np.int32)
+                args = np.array([a for _, a in prog], dtype=np.float64)
+                ok.append(L_.pft_ic_device_ok(C.byref(self.grid), len(prog), _ip(ops), _dp(args)))
+            if any(v < 0 for v in ok):
+                raise ValueError(f"pft_ic_device_ok: a bad icond program ({ok})")
+            device_ic = all(v == 1 for v in ok)   # one that is not device-exact: all on the host
+        if device_ic:
+            self.ic_where = "device"
+        if icond is not None and device_ic:
+            pass                # the programs run on the device after RK_MPI_SA_init (below)
+        elif icond is not None:
             # the parameter file's icond formulas, compiled by frontend.py (intertrack.c:1831-2012)
             for q, prog in icond:
                 ops = np.array([o for o, _ in prog], dtype=np.int32)
@@ -283,9 +301,18 @@ class Simulation:
             if rc:
                 raise RuntimeError(f"RK_MPI_SA_check_mem failed ({rc})")
         if device_ic:
-            # f1: the default Params' IC and the beads computed on the device (bit for bit the
-            # host's); the host array receives a copy, so every later call works as after a host IC
-            rc = L_.pft_solver_ic_default_device(1 if beads is not None else 0)
+            # f1: the default Params' IC (or the icond programs) and the beads computed on the device
+            # (bit for bit the host's); the host array receives a copy, so every later call works
+            # as after a host IC
+            if icond is not None:
+                qs = np.array([q for q, _ in icond], dtype=np.int32)
+                lens = np.array([len(prog) for _, prog in icond], dtype=np.int32)
+                ops = np.array([o for _, prog in icond for o, _ in prog], dtype=np.int32)
+                args = np.array([a for _, prog in icond for _, a in prog], dtype=np.float64)
+                rc = L_.pft_solver_ic_formulas_device(len(icond), _ip(qs), _ip(lens), _ip(ops), _dp(args),
+                                                      1 if beads is not None else 0)
+            else:
+                rc = L_.pft_solver_ic_default_device(1 if beads is not None else 0)
             if rc:
                 raise RuntimeError(f"pft_solver_ic_default_device failed ({rc}): {L_.pft_hip_last_error()}")
             if L_.pft_solver_download(C.byref(self.system)):

@@ -28,7 +28,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "../../include/pft_frontend.h"
 #include "../../include/pft_hip.h"
+#include "pft_ic_ops.h"
 #include "pft_tanh.h"
 
 #pragma clang fp contract(off)
@@ -1629,6 +1631,7 @@ struct IcDev {
   int nbeads;
   double u0, r2, s, R, reach2;
   unsigned int* unclean;
+  int overlay;           // 1: the beads over X's gl (an IC already in X, e.g. ic_prog_kernel's); u, p kept
 };
 
 // one thread per interior node: pft_model_ic_default (Params:9-21 as the reference's evaluator
@@ -1647,13 +1650,19 @@ __global__ __launch_bounds__(256) void ic_default_kernel(IcDev a)
   const double* Y = X + 4 * a.n1;
   const double* Z = Y + 4 * a.n2;
   const double* B = Z + 4 * a.n3;
-  const double p = (Z[2 * a.n3 + k] != 0.0 && X[2 * a.n1 + i] + Y[2 * a.n2 + j] < a.r2) ? 1.0 : 0.0;
-  double gl = Z[k];
-  gl = gl > Z[a.n3 + k] ? gl : Z[a.n3 + k];           // evmax (ee_wrapper.cc:246-250), in order
-  gl = gl > X[i] ? gl : X[i];
-  gl = gl > Y[j] ? gl : Y[j];
-  gl = gl > X[a.n1 + i] ? gl : X[a.n1 + i];
-  gl = gl > Y[a.n2 + j] ? gl : Y[a.n2 + j];
+  const long o = (long)(k + 1) * a.plane + r;
+  double p = 0.0, gl;
+  if (a.overlay) {
+    gl = a.x[2 * a.fs + o];
+  } else {
+    p = (Z[2 * a.n3 + k] != 0.0 && X[2 * a.n1 + i] + Y[2 * a.n2 + j] < a.r2) ? 1.0 : 0.0;
+    gl = Z[k];
+    gl = gl > Z[a.n3 + k] ? gl : Z[a.n3 + k];           // evmax (ee_wrapper.cc:246-250), in order
+    gl = gl > X[i] ? gl : X[i];
+    gl = gl > Y[j] ? gl : Y[j];
+    gl = gl > X[a.n1 + i] ? gl : X[a.n1 + i];
+    gl = gl > Y[a.n2 + j] ? gl : Y[a.n2 + j];
+  }
   if (a.nbeads) {
     const double x = X[3 * a.n1 + i], y = Y[3 * a.n2 + j], z = Z[3 * a.n3 + k];
     for (int t = a.poff[k]; t < a.poff[k + 1]; ++t) {
@@ -1666,14 +1675,46 @@ __global__ __launch_bounds__(256) void ic_default_kernel(IcDev a)
       if (gl < phf) gl = phf;
     }
   }
-  const long o = (long)(k + 1) * a.plane + r;
-  a.x[o] = a.u0;
-  a.x[a.fs + o] = p;
+  if (!a.overlay) {
+    a.x[o] = a.u0;
+    a.x[a.fs + o] = p;
+    a.xn[o] = a.u0;
+    a.xn[a.fs + o] = p;
+  }
   a.x[2 * a.fs + o] = gl;
-  a.xn[o] = a.u0;
-  a.xn[a.fs + o] = p;
   a.xn[2 * a.fs + o] = gl;
   if (gl != gl || (gl == 0.0 && signbit(gl))) atomicOr(a.unclean, 1u);
+}
+
+// f1 for any icond formula (pft_ic_compile): one thread per interior node runs the compiled
+// residual program (csrc/pft_ic_ops.h, the host's operators) on the node's u, p, gl in X and the
+// host-evaluated per-axis tables, into field q of X and XN -- as pft_ic_eval does on the host array
+struct IcProgDev {
+  double* x;
+  double* xn;
+  long fs;
+  int n1, n2, n3, plane, q, n;
+  const int* op;
+  const double* arg;
+  const int* taxis;
+  const long* toff;
+  const double* tval;
+  const unsigned char* terr;
+};
+
+__global__ __launch_bounds__(256) void ic_prog_kernel(IcProgDev a)
+{
+  const long n = (long)a.plane * a.n3;
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const int k = (int)(e / a.plane);
+  const int r = (int)(e - (long)k * a.plane);
+  const int j = r / a.n1, i = r - j * a.n1;
+  const long o = (long)(k + 1) * a.plane + r;
+  const double node[3] = {a.x[o], a.x[a.fs + o], a.x[2 * a.fs + o]};
+  const double v = pft_ic_run(a.n, a.op, a.arg, node, a.taxis, a.toff, a.tval, a.terr, i, j, k);
+  a.x[a.q * a.fs + o] = v;
+  a.xn[a.q * a.fs + o] = v;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2752,7 +2793,7 @@ int pft_slab_set_noise(pft_slab* s, const double* host_noise)
   return 0;
 }
 
-int pft_slab_ic_default(pft_slab* s, const pft_ic_tables* t, int* gl_unclean)
+static int slab_ic_tables(pft_slab* s, const pft_ic_tables* t, int overlay, int* gl_unclean)
 {
   if (!t || t->n1 != s->d.n1 || t->n2 != s->d.n2 || t->n3 != s->d.n3) return -2;
   const int n1 = t->n1, n2 = t->n2, n3 = t->n3, nb = t->nbeads;
@@ -2804,6 +2845,7 @@ int pft_slab_ic_default(pft_slab* s, const pft_ic_tables* t, int* gl_unclean)
     a.R = t->R;
     a.reach2 = t->reach2;
     a.unclean = du;
+    a.overlay = overlay;
     const long n = (long)s->plane * n3;
     ic_default_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s->stream>>>(a);
     e = hipGetLastError();
@@ -2816,6 +2858,76 @@ int pft_slab_ic_default(pft_slab* s, const pft_ic_tables* t, int* gl_unclean)
   (void)hipFree(du);
   if (e != hipSuccess) return fail(e, "pft_slab_ic_default");
   if (gl_unclean) *gl_unclean = hu ? 1 : 0;
+  return 0;
+}
+
+int pft_slab_ic_default(pft_slab* s, const pft_ic_tables* t, int* gl_unclean)
+{
+  return slab_ic_tables(s, t, 0, gl_unclean);
+}
+
+int pft_slab_ic_beads(pft_slab* s, const pft_ic_tables* t, int* gl_unclean)
+{
+  return slab_ic_tables(s, t, 1, gl_unclean);
+}
+
+int pft_slab_ic_program(pft_slab* s, int q, const pft_ic_prog* p, int clear)
+{
+  if (!p || q < 0 || q > 2 || p->n < 1) return -2;
+  hipError_t e = hipSuccess;
+  if (clear) {
+    // the host array the reference's loop fills starts zeroed: quantities not yet initialised read 0
+    e = hipMemsetAsync(s->buf[PFT_BUF_X], 0, sizeof(double) * 3 * (size_t)s->fs, s->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(s->buf[PFT_BUF_XN], 0, sizeof(double) * 3 * (size_t)s->fs, s->stream);
+  }
+  const size_t nt = (size_t)(p->ntab > 0 ? p->ntab : 1), nv = (size_t)(p->tab_len > 0 ? p->tab_len : 1);
+  const size_t bytes = sizeof(int) * p->n + sizeof(double) * p->n + sizeof(int) * nt + sizeof(long) * nt +
+                       sizeof(double) * nv + nv + 64;
+  std::vector<char> h(bytes, 0);
+  // one upload: [arg (n doubles)][tval (nv doubles)][toff (nt longs)][op (n ints)][taxis (nt ints)][terr]
+  size_t o = 0;
+  const size_t o_arg = o;  o += sizeof(double) * p->n;
+  const size_t o_val = o;  o += sizeof(double) * nv;
+  const size_t o_off = o;  o += sizeof(long) * nt;
+  const size_t o_op = o;   o += sizeof(int) * p->n;
+  const size_t o_ax = o;   o += sizeof(int) * nt;
+  const size_t o_err = o;
+  memcpy(&h[o_arg], p->arg, sizeof(double) * p->n);
+  memcpy(&h[o_op], p->op, sizeof(int) * p->n);
+  if (p->ntab > 0) {
+    memcpy(&h[o_val], p->tab_val, sizeof(double) * p->tab_len);
+    memcpy(&h[o_off], p->tab_off, sizeof(long) * p->ntab);
+    memcpy(&h[o_ax], p->tab_axis, sizeof(int) * p->ntab);
+    memcpy(&h[o_err], p->tab_err, p->tab_len);
+  }
+  char* d = nullptr;
+  if (e == hipSuccess) e = hipMalloc((void**)&d, bytes);
+  if (e == hipSuccess) e = hipMemcpyAsync(d, h.data(), bytes, hipMemcpyHostToDevice, s->stream);
+  if (e == hipSuccess) {
+    IcProgDev a;
+    a.x = s->buf[PFT_BUF_X];
+    a.xn = s->buf[PFT_BUF_XN];
+    a.fs = s->fs;
+    a.n1 = s->d.n1;
+    a.n2 = s->d.n2;
+    a.n3 = s->d.n3;
+    a.plane = s->plane;
+    a.q = q;
+    a.n = p->n;
+    a.arg = (const double*)(d + o_arg);
+    a.tval = (const double*)(d + o_val);
+    a.toff = (const long*)(d + o_off);
+    a.op = (const int*)(d + o_op);
+    a.taxis = (const int*)(d + o_ax);
+    a.terr = (const unsigned char*)(d + o_err);
+    const long n = (long)s->plane * s->d.n3;
+    ic_prog_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s->stream>>>(a);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+  if (d) (void)hipFree(d);
+  if (e != hipSuccess) return fail(e, "pft_slab_ic_program");
+  s->gl_keep = 0;
   return 0;
 }
 

@@ -12,6 +12,8 @@
  * rational correction, reconstruction by exponent arithmetic); the CPU test compares it with the
  * C library on 10^7 arguments (uniform on +-25, +-2, +-60 and log-uniform down to 2^-60): equal
  * bit for bit.  Division, multiplication, addition and the int conversion are IEEE on both sides.
+ * Attribution: the algorithm and its polynomial constants are fdlibm's (Sun Microsystems, 1993),
+ * as carried in the GNU C Library; none of /root/reference's code is involved.
  */
 #ifndef PFT_TANH_H
 #define PFT_TANH_H

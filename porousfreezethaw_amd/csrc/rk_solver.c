@@ -19,6 +19,7 @@
  * Solver state is per host thread (the reference's is per MPI process: one static instance).
  */
 #include "pft_internal.h"
+#include "../../include/pft_frontend.h"
 
 #include <math.h>
 #include <stdio.h>
@@ -685,30 +686,15 @@ int pft_solver_download(RK_MPI_S_SOLUTION * system)
 	return pft_slab_download_host(R.slab, PFT_BUF_X, system->x);
 }
 
-int pft_solver_ic_default_device(int with_beads)
+/* the common end of the device IC paths: every rank's outcome agreed (a rank that failed locally
+   still takes part, so that no other rank is left inside a collective: every rank returns the same,
+   most negative, code), then the ghost planes exchanged as at an upload and gl_keep agreed */
+static int ic_device_finish(int ret, int unclean)
 {
-	/* f1: the default Params' IC (and the glass beads) computed on the device into X and XN, bit
-	   for bit what pft_model_ic_default + PrecalculateData give on the host; the next
-	   pft_solve_ex(..., PFT_SOLVE_REUSE_DEVICE) starts from it.  Collective with nprocs > 1 (the
-	   ghost planes are exchanged, as at an upload, and the ranks agree on gl_keep). */
 	pft_comm * c = comm();
-	pft_ic_tables tb;
-	double * store = NULL;
-	int * istore = NULL, unclean = 0, rc, ret = 0;
-	long long u;
-	/* a rank that fails locally still takes part in the agreement below, so that no other rank is
-	   left inside a collective: every rank returns the same (most negative) code */
 	const long long FAILED = 1LL << 40;
-	if(R.max_n == 0) return -3;
-	if((rc = ensure_slab())) { R.last_status = rc; ret = PFT_SOLVE_DEVICE_ERROR; }
-	else if((rc = pft_model_ic_tables(&tb, with_beads, &store, &istore))) ret = rc;
-	else {
-		rc = pft_slab_ic_default(R.slab, &tb, &unclean);
-		if(rc) { R.last_status = rc; ret = PFT_SOLVE_DEVICE_ERROR; }
-	}
-	free(store);
-	free(istore);
-	u = ret ? FAILED - ret : unclean;
+	long long u = ret ? FAILED - ret : unclean;
+	int rc;
 	if(pft_comm_size(c) > 1 && (rc = pft_comm_allreduce_max_i64(c, &u))) {
 		R.last_status = rc;
 		return PFT_SOLVE_DEVICE_ERROR;
@@ -724,6 +710,65 @@ int pft_solver_ic_default_device(int with_beads)
 	R.device_valid = 1;
 	R.k1_keep = 0;
 	return 0;
+}
+
+int pft_solver_ic_default_device(int with_beads)
+{
+	/* f1: the default Params' IC (and the glass beads) computed on the device into X and XN, bit
+	   for bit what pft_model_ic_default + PrecalculateData give on the host; the next
+	   pft_solve_ex(..., PFT_SOLVE_REUSE_DEVICE) starts from it.  Collective with nprocs > 1 (the
+	   ghost planes are exchanged, as at an upload, and the ranks agree on gl_keep). */
+	pft_ic_tables tb;
+	double * store = NULL;
+	int * istore = NULL, unclean = 0, rc, ret = 0;
+	if(R.max_n == 0) return -3;
+	if((rc = ensure_slab())) { R.last_status = rc; ret = PFT_SOLVE_DEVICE_ERROR; }
+	else if((rc = pft_model_ic_tables(&tb, with_beads, &store, &istore))) ret = rc;
+	else {
+		rc = pft_slab_ic_default(R.slab, &tb, &unclean);
+		if(rc) { R.last_status = rc; ret = PFT_SOLVE_DEVICE_ERROR; }
+	}
+	free(store);
+	free(istore);
+	return ic_device_finish(ret, unclean);
+}
+
+int pft_solver_ic_formulas_device(int nprog, const int * qs, const int * lens, const int * ops,
+                                  const double * args, int with_beads)
+{
+	pft_grid g;
+	pft_ic_tables tb;
+	pft_ic_prog * pr;
+	double * store = NULL;
+	int * istore = NULL, unclean = 0, rc = 0, ret = 0, p, off = 0, ok = 1;
+	if(R.max_n == 0) return -3;
+	if(nprog < 1 || !qs || !lens || !ops || !args || pft_model_get_grid(&g)) return -2;
+	pr = (pft_ic_prog*)calloc(nprog, sizeof(pft_ic_prog));
+	if(!pr) return -1;
+	/* compile every program first: the decision (device or host) is the same on every rank (the
+	   programs are), and the device is not touched unless all of them compile */
+	for(p = 0; p < nprog && ok; p++) {
+		if(qs[p] < 0 || qs[p] > 2 || lens[p] < 1) { ok = 0; rc = -2; break; }
+		rc = pft_ic_compile(&g, lens[p], ops + off, args + off, &pr[p]);
+		off += lens[p];
+		if(rc) ok = 0;
+	}
+	if(!ok) {
+		for(p = 0; p < nprog; p++) pft_ic_prog_free(&pr[p]);
+		free(pr);
+		return rc;
+	}
+	if((rc = ensure_slab())) { R.last_status = rc; ret = PFT_SOLVE_DEVICE_ERROR; }
+	for(p = 0; p < nprog && !ret; p++)
+		if((rc = pft_slab_ic_program(R.slab, qs[p], &pr[p], p == 0))) { R.last_status = rc; ret = PFT_SOLVE_DEVICE_ERROR; }
+	for(p = 0; p < nprog; p++) pft_ic_prog_free(&pr[p]);
+	free(pr);
+	/* the beads over gl (PrecalculateData, equation.c:459-530), or only the gl scan without them */
+	if(!ret && (rc = pft_model_ic_tables(&tb, with_beads, &store, &istore))) ret = rc;
+	else if(!ret && (rc = pft_slab_ic_beads(R.slab, &tb, &unclean))) { R.last_status = rc; ret = PFT_SOLVE_DEVICE_ERROR; }
+	free(store);
+	free(istore);
+	return ic_device_finish(ret, unclean);
 }
 
 int pft_solver_eval_rhs(FLOAT t, const FLOAT * w, FLOAT * dw)

@@ -169,9 +169,9 @@ int main()
       printf("2D NoCU beside busy: busy %.3f ms, copies done at %.3f ms\n", ms(a0, a1), ms(a0, b1));
     }
   }
-  // correctness of the 1D NoCU copies
+  // correctness of the 1D NoCU copies (the fill ordered on the copy's own stream)
   {
-    CHK(hipMemset(dst, 0, sizeof(double) * 3 * fs));
+    CHK(hipMemsetAsync(dst, 0, sizeof(double) * 3 * fs, sB));
     CHK(copies(sB, hipMemcpyDeviceToDeviceNoCU));
     CHK(hipDeviceSynchronize());
     double h[4];
@@ -181,7 +181,38 @@ int main()
     CHK(hipMemcpy(&h[3], dst + fs + 2 * plane - 1, 8, hipMemcpyDeviceToHost));
     double want;
     memset(&want, 0x3c, 8);
-    printf("1D NoCU result %s\n", (h[0] == want && h[1] == want && h[2] == want && h[3] == want) ? "correct" : "WRONG");
+    printf("1D NoCU result %s (%a %a %a %a, want %a)\n", (h[0] == want && h[1] == want && h[2] == want && h[3] == want) ? "correct" : "WRONG",
+           h[0], h[1], h[2], h[3], want);
+  }
+  // the four copies on four streams (one SDMA queue each?), and eight half-copies on eight streams
+  {
+    hipStream_t ss[8];
+    for (int i = 0; i < 8; ++i) CHK(hipStreamCreateWithFlags(&ss[i], hipStreamNonBlocking));
+    hipEvent_t e8[8];
+    for (int i = 0; i < 8; ++i) CHK(hipEventCreate(&e8[i]));
+    for (int nst = 2; nst <= 8; nst *= 2) {
+      const int pieces = nst < 4 ? 4 : nst;           // 4 copies, or 8 halves
+      const long len = (pieces == 8 ? plane : 2 * plane);
+      for (int besides = 0; besides < 2; ++besides)
+        for (int rep = 0; rep < 3; ++rep) {
+          CHK(hipEventRecord(a0, sA));
+          if (besides) busy<<<nwg, 512, lds_bytes, sA>>>(in, out, n_per_wg, reps);
+          CHK(hipEventRecord(a1, sA));
+          for (int c = 0; c < pieces; ++c) {
+            hipStream_t st = ss[c % nst];
+            CHK(hipStreamWaitEvent(st, a0, 0));
+            const int f = (c / (pieces / 2)) & 1, half = c % (pieces / 2);
+            CHK(hipMemcpyAsync(dst + f * fs + 402 * plane + half * len, src + f * fs + 2 * plane + half * len, len * 8,
+                               hipMemcpyDeviceToDeviceNoCU, st));
+          }
+          for (int i = 0; i < nst; ++i) CHK(hipEventRecord(e8[i], ss[i]));
+          CHK(hipDeviceSynchronize());
+          double last = 0;
+          for (int i = 0; i < nst; ++i) last = ms(a0, e8[i]) > last ? ms(a0, e8[i]) : last;
+          printf("NoCU %d pieces on %d streams %s: busy %.3f ms, copies done at %.3f ms (%.1f GB/s)\n", pieces, nst,
+                 besides ? "beside busy" : "alone", ms(a0, a1), last, pieces * len * 8 / last / 1e6);
+        }
+    }
   }
   printf("done\n");
   return 0;

@@ -174,7 +174,7 @@ def test_solver_argument_codes():
     assert L.pft_solver_set_option(P.PFT_OPT_LAZY_ALLOC, 0) == 0
 
 
-@pytest.mark.parametrize("kw", [{"initial": np.zeros((3, 10, 10, 20))}, {"icond": []}, {"init_solver": False}])
+@pytest.mark.parametrize("kw", [{"initial": np.zeros((3, 10, 10, 20))}, {"init_solver": False}])
 def test_device_ic_rejects_conflicting_inputs(kw):
     """device_ic overwrites X/XN and the host copy: combining it with a caller's state, icond
     formulas or an uninitialised solver is refused up front (ValueError, also under python -O)"""
