@@ -79,3 +79,77 @@ def test_device_ic_g100_trajectory():
     sim.close()
     assert np.array_equal(x[:, -1], A["traj_m0_state0_top"])
     assert _sha(x) == meta["traj_m0_sha256"][0]
+
+
+# ---- f1 for any icond formula (pft_solver_ic_formulas_device) --------------------------------
+
+def _formula_sets():
+    import test_ic_compile as T
+    return [("published", f) for f in T._published()] + [("synthetic", f) for f in T.SYNTHETIC]
+
+
+def _formula_sim(formulas, dims, device_ic, nprocs=1, rank=0, beads=True):
+    import test_ic_compile as T
+    from porousfreezethaw_amd import frontend as FE
+    text = "".join(f'icond {k} = "{v}"\n' for k, v in formulas.items())
+    case = FE.load_params(text=T._minimal(text))
+    n1, n2, n3 = dims
+    return P.Simulation(n1, n2, n3, case.L, 0, case.params, nprocs=nprocs, rank=rank,
+                        beads=O.beads() if beads else None, icond=case.icond_programs(), tau=1.0,
+                        device_ic=device_ic)
+
+
+@pytest.mark.parametrize("which", range(10))
+@pytest.mark.parametrize("beads", [True, False])
+def test_device_formulas_equal_host(which, beads):
+    """every published formula set (and the synthetic ones of tests/test_ic_compile.py: every
+    operator class, multi-pass reads, math errors at some nodes) on the device, beads overlaid
+    there too: the host's IC (pft_ic_eval + PrecalculateData) bit for bit"""
+    sets = _formula_sets()
+    if which >= len(sets):
+        pytest.skip("fewer formula sets")
+    _, f = sets[which]
+    host = _formula_sim(f, (26, 18, 30), False, beads=beads)
+    a = host.interior()
+    assert host.ic_where == "host"
+    host.close()
+    dev = _formula_sim(f, (26, 18, 30), True, beads=beads)
+    assert dev.ic_where == "device"
+    b = dev.interior()
+    dev.close()
+    assert np.array_equal(a, b, equal_nan=True) and np.array_equal(np.signbit(a), np.signbit(b))
+
+
+@pytest.mark.parametrize("nprocs", [3])
+def test_device_formulas_multislab(nprocs):
+    """each slab evaluates its own planes (z tables with its first_row): the global field is the
+    single-slab host IC"""
+    f = _formula_sets()[0][1]
+    host = _formula_sim(f, (24, 20, 33), False)
+    ref = host.interior()
+    host.close()
+    out = M.loopback_run(nprocs, lambda r: _formula_sim(f, (24, 20, 33), True, nprocs, r), lambda sim: sim.interior())
+    assert np.array_equal(np.concatenate(out, axis=1), ref)
+
+
+def test_device_formulas_default_params_g100():
+    """the default Params' formulas (Params:9-21) compiled for the device at g100 (BASELINE
+    configs[0]), beads overlaid on the device: the reference's own IC digest -- the general path
+    reproduces what the fixed-function kernel and the reference give"""
+    import test_ic_compile as T
+    from porousfreezethaw_amd import frontend as FE
+    meta, _ = O.load_case("g100")
+    base, Pm, info = M.full_size_case(100, 0)
+    ev = FE.Evaluator()
+    for k, v in base.items():
+        if isinstance(v, (int, float)):
+            ev.define(k, float(v))
+    case = FE.Case.__new__(FE.Case)
+    case.ev, case.icond = ev, T._published()[-1]     # the default Params' formulas
+    sim = P.Simulation(info["n1"], info["n2"], info["n3"], (info["L1"], info["L2"], info["L3"]), 0, Pm,
+                       beads=O.beads(), icond=case.icond_programs(), tau=1.0, tau_min=info["tau_min"],
+                       delta=info["delta"], device_ic=True)
+    assert sim.ic_where == "device"
+    x = sim.interior()
+    sim.close()
+    assert _sha(x) == meta["ic_sha256"]

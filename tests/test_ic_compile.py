@@ -6,23 +6,19 @@ tables (the C library's own values) and leaves a residual program of operators t
 evaluates as the host does.  pft_ic_eval_compiled runs that residual program with the device's
 operator code compiled for the host; it must give pft_ic_eval's bits (the host path, pinned to the
 reference's IC by tests/test_frontend.py) at every node -- for every formula the reference's
-published cases use (read from /root/reference's results/ archives where present), the default
+published cases use (tests/golden/icond_published.json, from its results/ archives), the default
 Params, multi-pass formulas over u/p/gl, math errors at some nodes (0 there, as the reference's
 Eval()), and on several Z-slabs.  The GPU test (tests/test_device_ic.py) runs the same programs
 through ic_prog_kernel."""
 import ctypes as C
-import glob
+import json
 import os
-import re
-import tarfile
 
 import numpy as np
 import pytest
 
 import porousfreezethaw_amd as P
 from porousfreezethaw_amd import frontend as FE
-
-REF_APP = "/root/reference/apps/intertrack-hybrid-S-freezing"
 
 # formulas written for this test: every operator class, multi-pass reads, per-node math errors
 SYNTHETIC = [
@@ -63,29 +59,11 @@ def _programs(formulas):
 
 
 def _published():
-    out = []
-    for arc in sorted(glob.glob(os.path.join(REF_APP, "results", "*", "*.tgz"))):
-        with tarfile.open(arc) as tf:
-            for m in tf.getmembers():
-                if m.isfile() and m.name.endswith("/Params"):
-                    t = tf.extractfile(m).read().decode("latin-1")
-                    f = {}
-                    for line in t.splitlines():
-                        mm = re.match(r'\s*icond\s+(\w+)\s*=\s*"([^"]*)"', line)
-                        if mm:
-                            f[mm.group(1)] = mm.group(2)
-                    if len(f) == 3 and f not in out:
-                        out.append(f)
-    dp = os.path.join(REF_APP, "Params")
-    if os.path.exists(dp):
-        f = {}
-        for line in open(dp).read().splitlines():
-            mm = re.match(r'\s*icond\s+(\w+)\s*=\s*"([^"]*)"', line)
-            if mm:
-                f[mm.group(1)] = mm.group(2)
-        if len(f) == 3 and f not in out:
-            out.append(f)
-    return out
+    """the distinct formula sets of the reference's published cases and its default Params
+    (tests/golden/icond_published.json, made from the reference's files by gen_icond.py)"""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "icond_published.json")
+    d = json.load(open(path))
+    return [c["icond"] for c in d["published"]] + [d["default"]]
 
 
 def _both(progs, n1, n2, total_n3, nprocs, rank):
@@ -119,9 +97,7 @@ def test_compiled_equals_host_synthetic(which, dims, nprocs):
 
 def test_compiled_equals_host_published():
     cases = _published()
-    if not cases:
-        pytest.skip("reference result archives not available here")
-    assert len(cases) >= 4
+    assert len(cases) >= 5
     for f in cases:
         progs = _programs(f)
         for nprocs, r in ((1, 0), (4, 2)):
