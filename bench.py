@@ -94,7 +94,7 @@ def parse():
     ap.add_argument("--host-boundary", action="store_true",
                     help="timed call is one RK_MPI_SA_solve-style call: x copied host->device at entry "
                          "and back at exit (PCIe-inclusive rate; never the headline value)")
-    ap.add_argument("--transport", choices=("auto", "ipc", "rccl"), default="auto",
+    ap.add_argument("--transport", choices=("auto", "ipc", "ipc-ce", "rccl"), default="auto",
                     help="N>1 (and --self-exchange) inter-slab transport (pft_comm.h): ipc = IPC-mapped "
                          "neighbour slabs, boundary planes stored into their ghost planes + flag words; "
                          "rccl = ncclSend/ncclRecv on a priority stream beside the interior sweep; auto "
@@ -463,11 +463,14 @@ def make_comm(L, transport, world, rank, dev, dist, fallback=True):
     staged receive -- so that an N > 1 run still measures, and checks its parity, rather than
     ending; the JSON line then names the transport that ran."""
     comm = C.c_void_p()
-    if transport == "ipc":
+    if transport in ("ipc", "ipc-ce"):
         name = [f"/pft_bench_{os.getpid()}_{int(time.time() * 1e6) % 10**9}"]
         if dist is not None:
             dist.broadcast_object_list(name, src=0)
         rc = L.pft_comm_init_ipc(C.byref(comm), world, rank, name[0].encode(), dev)
+        if rc == 0 and transport == "ipc-ce":
+            # the halo planes on the copy engines beside the interior launch (pft_comm_set_copy_engine)
+            assert L.pft_comm_set_copy_engine(comm, 1) == 0
     else:
         uid = (C.c_char * 128)()
         if rank == 0:

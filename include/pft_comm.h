@@ -63,6 +63,15 @@ int pft_comm_set_self_exchange(pft_comm * c, int on);
 /* 1: the ipc transport exchanges halos (more than one rank, or the self exchange): every stage is
    one launch over all planes followed by the stream-ordered put + wait (no boundary split) */
 int pft_comm_device_halo(const pft_comm * c);
+/* 1: each launch whose output is exchanged runs its boundary planes first and the exchange goes
+   beside the interior launch (pft_comm_halo_start ... interior ... pft_comm_halo_finish): RCCL,
+   loopback, and ipc on the copy engines; 0: one launch, then the exchange (ipc with put kernels) */
+int pft_comm_boundary_first(const pft_comm * c);
+/* ipc, before a slab is attached: 1 = the exchange on the copy engines (SDMA copies of the planes
+   and 8-byte copies raising the flags on the comm stream, pft_slab_halo_put_ce) beside the interior
+   launch, instead of a put kernel after the whole-slab launch; env PFT_IPC_CE=1 sets it at init */
+int pft_comm_set_copy_engine(pft_comm * c, int on);
+int pft_comm_copy_engine(const pft_comm * c);
 int pft_comm_size(const pft_comm * c);
 const char * pft_comm_kind(const pft_comm * c);
 

@@ -278,6 +278,11 @@ int pft_slab_halo_put(pft_slab * s, int role, int f0, int f1, unsigned long long
 /* the same with deep = 1: also planes 2 and n3-1 into the neighbours' far ghost planes (the pair
    kernels' two-plane halo) */
 int pft_slab_halo_put2(pft_slab * s, int role, int f0, int f1, int deep, unsigned long long seq);
+/* the same put on the copy engines (SDMA, hipMemcpyDeviceToDeviceNoCU) from the slab's comm stream,
+   ordered after the work already on the compute stream: the planes and then the neighbours' flags
+   (8-byte copies), no kernel -- beside the interior launch that follows on the compute stream.
+   The receiver's side is pft_slab_halo_wait as for halo_put2. */
+int pft_slab_halo_put_ce(pft_slab * s, int role, int f0, int f1, int deep, unsigned long long seq);
 /* far ghost plane of buffer `which`, field q: side 0 = two planes below the slab (the neighbour
    below's plane n3' - 1; plane -1 of the field), side 1 = two above (the neighbour above's plane
    2; plane n3 + 2) */

@@ -139,6 +139,9 @@ def lib():
         L.pft_comm_init_loopback.argtypes = [C.POINTER(C.c_void_p), C.c_int]
         L.pft_comm_init_ipc.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_char_p, C.c_int]
         L.pft_comm_device_halo.argtypes = [C.c_void_p]
+        L.pft_comm_boundary_first.argtypes = [C.c_void_p]
+        L.pft_comm_copy_engine.argtypes = [C.c_void_p]
+        L.pft_comm_set_copy_engine.argtypes = [C.c_void_p, C.c_int]
         L.pft_comm_loopback_rank.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
         L.pft_comm_set_current.argtypes = [C.c_void_p]
         L.pft_comm_destroy.argtypes = [C.c_void_p]

@@ -81,6 +81,8 @@ struct pft_comm {
   unsigned long long hseq;   // host collective rounds so far (identical on every rank)
   unsigned long long dseq;   // device halo exchanges so far (identical on every rank)
   double timeout_s;
+  int ce;                    // ipc: the halo planes go on the copy engines beside the interior launch
+                             // (pft_comm_set_copy_engine; env PFT_IPC_CE)
   void* bcast_pinned;        // rccl: pinned host staging of pft_comm_bcast
   // rccl: every host wait on RCCL work is bounded (PFT_COMM_TIMEOUT, default 300 s) and watches
   // ncclCommGetAsyncError; on expiry or an error the communicator is aborted (ncclCommAbort) and
@@ -289,6 +291,8 @@ int pft_comm_init_ipc(pft_comm** c, int nranks, int rank, const char* name, int 
   m->device = device;
   const char* to = getenv("PFT_IPC_TIMEOUT");
   m->timeout_s = to ? atof(to) : 300.0;
+  const char* ec = getenv("PFT_IPC_CE");
+  m->ce = ec ? atoi(ec) != 0 : 0;
   snprintf(m->shm_name, sizeof(m->shm_name), "%s", name);
   const size_t bytes = sizeof(IpcShared);
   int fd = -1;
@@ -418,6 +422,17 @@ int pft_comm_set_self_exchange(pft_comm* c, int on)
   return 0;
 }
 int pft_comm_device_halo(const pft_comm* c) { return c && c->kind == KIND_IPC && (c->size > 1 || c->self_x); }
+int pft_comm_boundary_first(const pft_comm* c)
+{
+  return pft_comm_splits(c) && !(c->kind == KIND_IPC && !c->ce);
+}
+int pft_comm_set_copy_engine(pft_comm* c, int on)
+{
+  if (!c || c->kind != KIND_IPC || c->slab) return -2;
+  c->ce = on ? 1 : 0;
+  return 0;
+}
+int pft_comm_copy_engine(const pft_comm* c) { return c && c->kind == KIND_IPC && c->ce; }
 int pft_comm_size(const pft_comm* c) { return c ? c->size : 1; }
 const char* pft_comm_kind(const pft_comm* c)
 {
@@ -506,9 +521,16 @@ static int halo_start(pft_comm* c, int buf, int f0, int f1, bool deep = false)
   // which a single slab never reads (mirror bottom wall, Dirichlet top)
   const int pb = c->self_x ? c->rank : c->rank - 1, pa = c->self_x ? c->rank : c->rank + 1;
   if (c->kind == KIND_IPC) {
+    const unsigned long long seq = ++c->dseq;
+    if (c->ce) {
+      // copy engines: the planes and the flags go out on the comm stream, beside whatever the
+      // compute stream runs next (the interior launch); halo_finish waits for our own flags
+      int rc = pft_slab_halo_put_ce(s, buf, f0, f1, deep ? 1 : 0, seq);
+      if (!rc) c->pending = 1;
+      return rc;
+    }
     // stream-ordered on the compute stream: put (boundary planes into the neighbours' ghost
     // planes, then their flags), then wait for our own flags
-    const unsigned long long seq = ++c->dseq;
     int rc = pft_slab_halo_put2(s, buf, f0, f1, deep ? 1 : 0, seq);
     return rc ? rc : pft_slab_halo_wait(s, seq);
   }
@@ -580,6 +602,7 @@ int pft_comm_halo_finish(pft_comm* c)
 {
   if (!pft_comm_splits(c) || !c->pending) return 0;
   c->pending = 0;
+  if (c->kind == KIND_IPC) return pft_slab_halo_wait(c->slab, c->dseq);
   HCHK(hipStreamWaitEvent((hipStream_t)pft_slab_stream(c->slab), c->ev_done, 0));
   return 0;
 }

@@ -1942,6 +1942,13 @@ struct pft_slab {
   unsigned long long* sig;       // flag words written by the neighbours: [0] from below, [1] from
                                  // above (monotonic exchange sequence numbers); [8] put counter
   double* rbuf;                  // staged receive buffer (uncached, 2 x 12 planes; pft_slab_ipc_export)
+  // copy-engine puts (pft_slab_halo_put_ce): the flags are raised by 8-byte SDMA copies from this
+  // device table of sequence numbers (seq_base + 1 .. seq_base + PFT_SEQTAB), refilled from the
+  // pinned halves seqhost[] when an exchange's number leaves it
+  unsigned long long* seqtab;
+  unsigned long long* seqhost;
+  unsigned long long seq_base;
+  int seq_half;
   int put_role, put_f0, put_f1, put_deep;   // the exchange the last halo_put2 sent (its wait receives it)
   SlabPeer peer[2];              // [0] the neighbour below, [1] above
   int drop_puts;                 // fault injection: halo puts and flag raises skipped (PFT_IPC_DROP_PUTS)
@@ -2249,6 +2256,8 @@ int pft_slab_destroy(pft_slab* s)
     if (s->buf0[b]) (void)hipFree(s->buf0[b]);
   if (s->sig) (void)hipFree(s->sig);
   if (s->rbuf) (void)hipFree(s->rbuf);
+  if (s->seqtab) (void)hipFree(s->seqtab);
+  if (s->seqhost) (void)hipHostFree(s->seqhost);
   if (s->staging) (void)hipFree(s->staging);
   if (s->noise) (void)hipFree(s->noise);
   for (int st = 0; st < 6; ++st)
@@ -3592,6 +3601,74 @@ int pft_slab_halo_put2(pft_slab* s, int role, int f0, int f1, int deep, unsigned
   halo_put_kernel<<<blocks, 256, 0, s->stream>>>(a);
   HIPCHK(hipGetLastError());
   return pft_slab_halo_signal(s, seq);
+}
+
+#define PFT_SEQTAB 4096
+
+// The ipc exchange on the copy engines (SDMA): after the launch that wrote the boundary planes (an
+// event on the compute stream), the comm stream copies them into the neighbours' ghost (and far
+// ghost) planes -- or their receive buffers when staged -- with hipMemcpyDeviceToDeviceNoCU, then
+// raises the neighbours' flags with 8-byte copies of the sequence number from seqtab.  No kernel:
+// the copies need no CU, so they run beside the interior launch that holds every CU's LDS (a blit
+// kernel, or RCCL's, waits for that launch to end: profiles/r05_sdma_probe.txt).  The receiver
+// side is unchanged (pft_slab_halo_wait: the compute stream waits for the flags; staged: the
+// receive kernel), so a sender may use either put.
+int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsigned long long seq)
+{
+  if (role < 0 || role >= PFT_BUF_COUNT || f0 < 0 || f1 > 3 || f1 <= f0 || seq == 0) return -2;
+  if (s->ipc_poisoned) return slab_poisoned(s, "pft_slab_halo_put_ce");
+  s->put_role = role;
+  s->put_f0 = f0;
+  s->put_f1 = f1;
+  s->put_deep = deep ? 1 : 0;
+  if (s->drop_puts) return 0;
+  if (!s->peer[0].on && !s->peer[1].on) return 0;
+  if (!s->seqtab) {
+    HIPCHK(hipMalloc((void**)&s->seqtab, sizeof(unsigned long long) * PFT_SEQTAB));
+    HIPCHK(hipHostMalloc((void**)&s->seqhost, 2 * sizeof(unsigned long long) * PFT_SEQTAB, hipHostMallocDefault));
+    s->seq_base = ~0ULL;
+  }
+  if (s->seq_base == ~0ULL || seq <= s->seq_base || seq > s->seq_base + PFT_SEQTAB) {
+    // the next block of sequence numbers, from the pinned half not used by the previous refill
+    // (that one's copy is PFT_SEQTAB exchanges old: complete)
+    s->seq_base = (seq - 1) / PFT_SEQTAB * PFT_SEQTAB;
+    s->seq_half ^= 1;
+    unsigned long long* h = s->seqhost + (size_t)s->seq_half * PFT_SEQTAB;
+    for (int i = 0; i < PFT_SEQTAB; ++i) h[i] = s->seq_base + 1 + i;
+    HIPCHK(hipMemcpyAsync(s->seqtab, h, sizeof(unsigned long long) * PFT_SEQTAB, hipMemcpyHostToDevice, s->comm));
+  }
+  HIPCHK(hipEventRecord(s->ev_order[0], s->stream));
+  HIPCHK(hipStreamWaitEvent(s->comm, s->ev_order[0], 0));
+  const int ph = s->phys[role];
+  const long P = s->plane, n3 = s->d.n3;
+  const long slot = (long)(seq & 1) * 12 * P;
+  const size_t pb = sizeof(double) * (size_t)P;
+  for (int side = 0; side < 2; ++side) {
+    const SlabPeer& p = s->peer[side];
+    if (!p.on) continue;
+    for (int q = f0; q < f1; ++q) {
+      const double* src = s->buf[role] + q * s->fs;
+      if (!p.staged) {
+        // below: our planes 1 (, 2) into its ghost n3'+1 (, far n3'+2); above: our planes (n3-1,) n3
+        // into its (far -1,) ghost 0 -- contiguous on both ends
+        double* dst = side == 0 ? p.base[ph] + q * p.fs + (p.n3 + 1) * P : p.base[ph] + q * p.fs - (deep ? P : 0);
+        const double* sp = side == 0 ? src + P : src + (deep ? n3 - 1 : n3) * P;
+        HIPCHK(hipMemcpyAsync(dst, sp, (deep ? 2 : 1) * pb, hipMemcpyDeviceToDeviceNoCU, s->comm));
+      } else {
+        // its receive buffer [slot][side][depth][field][plane]: the neighbour below receives our
+        // planes as "from above" (side 1), the one above as "from below" (side 0)
+        for (int d = 0; d < (deep ? 2 : 1); ++d) {
+          double* dst = p.rbuf + slot + ((long)((side == 0 ? 1 : 0) * 2 + d) * 3 + q) * P;
+          const double* sp = side == 0 ? src + (1 + d) * P : src + (n3 - d) * P;
+          HIPCHK(hipMemcpyAsync(dst, sp, pb, hipMemcpyDeviceToDeviceNoCU, s->comm));
+        }
+      }
+    }
+  }
+  const unsigned long long* sv = s->seqtab + (seq - 1 - s->seq_base);
+  if (s->peer[0].on) HIPCHK(hipMemcpyAsync(s->peer[0].sig + 1, sv, 8, hipMemcpyDeviceToDeviceNoCU, s->comm));
+  if (s->peer[1].on) HIPCHK(hipMemcpyAsync(s->peer[1].sig + 0, sv, 8, hipMemcpyDeviceToDeviceNoCU, s->comm));
+  return 0;
 }
 
 int pft_slab_halo_signal(pft_slab* s, unsigned long long seq)

@@ -266,10 +266,11 @@ static int do_stage(int stage, double ts, double coef, double h, long * launches
 	if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 0);
 	if(R.deep) {
 		/* pair path between slabs: the output's two-plane halo (the next pair kernel evaluates its
-		   stage A on the ghost planes too).  RCCL: the two planes at each end first, their exchange
-		   on the comm stream beside the interior launch; ipc: the whole slab, then the put. */
+		   stage A on the ghost planes too).  RCCL and ipc on the copy engines: the two planes at each
+		   end first, their exchange on the comm stream beside the interior launch; ipc with put
+		   kernels: the whole slab, then the put. */
 		n3 = R.slab_grid.n3;
-		if(!pft_comm_device_halo(c) && n3 >= 5) {
+		if(pft_comm_boundary_first(c) && n3 >= 5) {
 			if((rc = run1(stage, ts, coef, h, PFT_K_BOUNDARY2, 0))) return rc;
 			if((rc = pft_comm_halo_start_deep(c, out_buf, 0, nfields))) return rc;
 			if((rc = run1(stage, ts, coef, h, 2, n3-2))) return rc;
@@ -282,7 +283,7 @@ static int do_stage(int stage, double ts, double coef, double h, long * launches
 		if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
 		return pft_comm_halo_deep(c, out_buf, 0, nfields);
 	}
-	if(pft_comm_device_halo(c)) {
+	if(pft_comm_device_halo(c) && !pft_comm_boundary_first(c)) {
 		/* ipc: the whole slab in one launch, then (stream-ordered) the boundary planes into the
 		   neighbours' ghost planes and the wait for theirs in ours */
 		(*launches)++;
@@ -318,9 +319,10 @@ static int do_pair(int first, double ta, double tb, double h, double coef, long 
 	const int out_buf = first == 2 ? PFT_BUF_K3 : PFT_BUF_XN, n3 = R.slab_grid.n3;
 	int rc;
 	if(R.tstep) pft_slab_timing_mark(R.slab, first+1, 0);
-	if(R.deep && !pft_comm_device_halo(c) && n3 >= 5) {
-		/* between slabs over RCCL: the two planes at each end first, their exchange (K3, or x(t+h):
-		   gl only where stored) beside the interior launch, which reads no ghost plane */
+	if(R.deep && pft_comm_boundary_first(c) && n3 >= 5) {
+		/* between slabs over RCCL or the copy engines: the two planes at each end first, their
+		   exchange (K3, or x(t+h): gl only where stored) beside the interior launch, which reads no
+		   ghost plane */
 		const int nf = pft_slab_stage_fields(R.slab, first+1);
 		*launches += 2;
 		if((rc = pft_slab_pair_range(R.slab, first, ta, tb, h, coef, PFT_K_BOUNDARY2, 0))) return rc;

@@ -205,3 +205,93 @@ def test_lost_ipc_halo_ends_in_device_error_not_a_hang(tmp_path):
         assert int(r["rc2"]) == P.PFT_SOLVE_DEVICE_ERROR
         assert int(r["status2"]) in (-5000, -5002)
         assert float(r["seconds2"]) < 60
+
+
+# ---- the exchange on the copy engines (PFT_IPC_CE=1: pft_slab_halo_put_ce) --------------------
+
+@pytest.mark.parametrize("nranks,pair,staged,ce_ranks", [(2, 2, 0, (0, 1)), (3, 2, 0, (0, 1, 2)), (3, 2, 1, (0, 1, 2)),
+                                                          (2, 0, 0, (0, 1)), (3, 0, 1, (0, 1, 2)),
+                                                          (3, 2, 0, (1,))])
+def test_g20_processes_copy_engine_equal_reference(tmp_path, nranks, pair, staged, ce_ranks):
+    """the boundary planes first, their exchange as SDMA copies and 8-byte flag copies on the comm
+    stream beside the interior launch, the receiver's flag wait before the next launch: golden g20
+    bit for bit with the pair kernels (two-plane halo) and one launch per stage, direct and staged.
+    ce_ranks (1,): only the middle rank puts on the copy engines, its neighbours with the put
+    kernel -- the receiving side is the same for both"""
+    meta, A = O.load_case("g20")
+    times = meta["traj_times"][:2]
+    env = {r: dict({"PFT_IPC_CE": "1"} if r in ce_ranks else {}, **({"PFT_IPC_STAGED": "1"} if staged else {}))
+           for r in range(nranks)}
+    res = _run_ranks(tmp_path, nranks, rank_env=env, case="g20", times=times, tile=2, pair=pair)
+    for r in res:
+        assert int(r["path"]) == 1 and int(r["pairs"]) == (1 if pair else 0)
+    for i in range(len(times)):
+        ref = meta["traj_m0"][i]
+        for r in res:
+            t, h, s, st, rc = r["rows"][i]
+            assert (t.hex(), h.hex(), int(s), int(st), int(rc)) == \
+                (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(), ref[2], ref[3], ref[4])
+        full = np.concatenate([r["states"][i] for r in res], axis=1)
+        assert np.array_equal(full, A[f"traj_m0_state{i}"])
+
+
+@pytest.mark.parametrize("staged", [0, 1])
+def test_400_processes_copy_engine_equal_one_slab(tmp_path, staged):
+    """400^3 over 2 processes with the pair kernels, the exchange on the copy engines"""
+    steps = 10
+    base, Pm, info = M.full_size_case(400, 0)
+    sim = P.Simulation(info["n1"], info["n2"], info["n3"], (info["L1"], info["L2"], info["L3"]), 0, Pm,
+                       beads=O.beads(), tau=1.0, tau_min=info["tau_min"], delta=info["delta"])
+    assert sim.solve_ex(1e9, steps, 0) == 2
+    got = (sim.t, sim.h, sim.system.steps, sim.system.steps_total)
+    x = sim.interior()
+    sim.close()
+    env = {r: dict({"PFT_IPC_CE": "1"}, **({"PFT_IPC_STAGED": "1"} if staged else {})) for r in range(2)}
+    res = _run_ranks(tmp_path, 2, rank_env=env, case="default", grid_nodes=400, times=[1e9], steps=steps, pair=2)
+    for r in res:
+        assert int(r["pairs"]) == 1
+        t, h, s, st, rc = r["rows"][0]
+        assert (t, h, int(s), int(st), int(rc)) == got + (2,)
+    assert np.array_equal(np.concatenate([r["states"][0] for r in res], axis=1), x)
+
+
+@pytest.mark.parametrize("staged", [0, 1])
+@pytest.mark.parametrize("pair", [2, 0])
+def test_ipc_copy_engine_self_exchange_equals_reference(pair, staged, monkeypatch):
+    """one process exchanging with itself on the copy engines (bench.py --self-exchange
+    --transport ipc-ce): every exchange's SDMA copies, flag copies and waits run"""
+    monkeypatch.setenv("PFT_IPC_CE", "1")
+    if staged:
+        monkeypatch.setenv("PFT_IPC_STAGED", "1")
+    meta, A = O.load_case("g20")
+    Pm, info = O.params_from_meta(meta)
+    comm = P.comm_init_ipc(1, 0, f"/pft_ceselfx_{os.getpid()}_{uuid.uuid4().hex[:12]}")
+    P.lib().pft_solver_set_option(P.PFT_OPT_PAIR, pair)
+    try:
+        assert P.lib().pft_comm_set_self_exchange(comm, 1) == 0
+        assert P.lib().pft_comm_copy_engine(comm) == 1 and P.lib().pft_comm_boundary_first(comm) == 1
+        sim = P.Simulation(info["n1"], info["n2"], info["n3"], (info["L1"], info["L2"], info["L3"]), 0, Pm,
+                           initial=A["traj_m0_ic"], tau=1.0, tau_min=info["tau_min"], delta=info["delta"], tile=2)
+        for i, T in enumerate(meta["traj_times"][:2]):
+            rc = sim.solve(T)
+            ref = meta["traj_m0"][i]
+            assert (sim.t.hex(), sim.h.hex(), sim.system.steps, sim.system.steps_total, rc) == \
+                (float.fromhex(ref[0]).hex(), float.fromhex(ref[1]).hex(), ref[2], ref[3], ref[4])
+            assert np.array_equal(sim.interior(), A[f"traj_m0_state{i}"])
+        assert sim.stats().pairs == (1 if pair else 0)
+        sim.close()
+    finally:
+        P.lib().pft_solver_set_option(P.PFT_OPT_PAIR, 1)
+        P.comm_destroy(comm)
+
+
+def test_lost_copy_engine_halo_ends_in_device_error(tmp_path):
+    """as test_lost_ipc_halo_ends_in_device_error_not_a_hang, with the copy-engine put"""
+    env = {0: {"PFT_IPC_CE": "1"}, 1: {"PFT_IPC_CE": "1", "PFT_IPC_DROP_PUTS": "1"}}
+    res = _run_ranks(tmp_path, 2, timeout=240, case="g20", times=[36.0], raw_rc=True, ipc_timeout="5",
+                     second_call=True, rank_env=env)
+    for r in res:
+        assert int(r["rc"]) == P.PFT_SOLVE_DEVICE_ERROR
+        assert int(r["status"]) in (-5000, -5002)
+        assert float(r["seconds"]) < 60
+        assert int(r["rc2"]) == P.PFT_SOLVE_DEVICE_ERROR
