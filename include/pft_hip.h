@@ -283,6 +283,12 @@ int pft_slab_halo_put2(pft_slab * s, int role, int f0, int f1, int deep, unsigne
    (8-byte copies), no kernel -- beside the interior launch that follows on the compute stream.
    The receiver's side is pft_slab_halo_wait as for halo_put2. */
 int pft_slab_halo_put_ce(pft_slab * s, int role, int f0, int f1, int deep, unsigned long long seq);
+/* 1: a launch of the boundary planes (k_begin PFT_K_BOUNDARY / PFT_K_BOUNDARY2) runs on a stream of
+   its own at the greatest priority, beside the interior launch that follows on the compute stream,
+   instead of before it; the copy-engine exchange starts when it ends, and pft_slab_halo_wait makes
+   the compute stream wait for it before the next launch (its planes are that launch's input).  The
+   boundary launch takes the second set of error-norm shards. */
+int pft_slab_set_boundary_stream(pft_slab * s, int on);
 /* far ghost plane of buffer `which`, field q: side 0 = two planes below the slab (the neighbour
    below's plane n3' - 1; plane -1 of the field), side 1 = two above (the neighbour above's plane
    2; plane n3 + 2) */

@@ -487,6 +487,7 @@ static int ipc_attach(pft_comm* c, pft_slab* s)
   }
   // the slots are reused by the next attach only after everyone has read them
   if ((rc = ipc_round(c, nullptr, 0, nullptr, 0, &recs))) return rc;
+  if ((rc = pft_slab_set_boundary_stream(s, c->ce))) return rc;
   c->slab = s;
   return 0;
 }

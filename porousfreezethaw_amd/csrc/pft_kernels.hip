@@ -1949,6 +1949,13 @@ struct pft_slab {
   unsigned long long* seqhost;
   unsigned long long seq_base;
   int seq_half;
+  // boundary launches on their own stream (pft_slab_set_boundary_stream; the copy-engine exchange):
+  // a launch of the boundary planes (PFT_K_BOUNDARY/2) runs on `bnd` beside the interior launch on
+  // the compute stream instead of before it; the exchange waits for ev_bnd, and so does the compute
+  // stream before the next launch (pft_slab_halo_wait)
+  int bnd_mode, bnd_pending, ce_streams;
+  hipStream_t bnd;
+  hipEvent_t ev_bnd, ev_pre, ev_copy;
   int put_role, put_f0, put_f1, put_deep;   // the exchange the last halo_put2 sent (its wait receives it)
   SlabPeer peer[2];              // [0] the neighbour below, [1] above
   int drop_puts;                 // fault injection: halo puts and flag raises skipped (PFT_IPC_DROP_PUTS)
@@ -2076,8 +2083,14 @@ static int slab_timed_out(pft_slab* s, const char* what)
 {
   static const unsigned long long released[2] = {~0ULL >> 1, ~0ULL >> 1};
   s->ipc_poisoned = 1;
-  (void)hipMemcpyAsync(s->sig, released, sizeof(released), hipMemcpyHostToDevice, s->side);
-  (void)hipStreamSynchronize(s->side);
+  // on a stream of its own: the slab's other streams may hold copies waiting (through events) for
+  // the blocked compute stream (the copy-engine exchange)
+  hipStream_t rel = nullptr;
+  if (hipStreamCreateWithFlags(&rel, hipStreamNonBlocking) == hipSuccess) {
+    (void)hipMemcpyAsync(s->sig, released, sizeof(released), hipMemcpyHostToDevice, rel);
+    (void)hipStreamSynchronize(rel);
+    (void)hipStreamDestroy(rel);
+  }
   (void)hipStreamSynchronize(s->stream);
   (void)hipGetLastError();
   snprintf(g_err, sizeof(g_err), "%s: no halo from an ipc neighbour within %.0f s (PFT_IPC_TIMEOUT)", what,
@@ -2219,7 +2232,9 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
   if (e == hipSuccess) memset(s->gate_pin, 0, 32 * PFT_GATE_SLOTS);
   if (e == hipSuccess) e = hipMalloc((void**)&s->gate_dev, 32 * PFT_GATE_SLOTS);
   if (e == hipSuccess) e = hipMemsetAsync(s->gate_dev, 0, 32 * PFT_GATE_SLOTS, s->stream);
-  const size_t cnt_bytes = 64 + sizeof(EpsShard) * PFT_EPS_SHARDS;
+  // two sets of error-norm shards: a boundary launch uses the second, so that it may run beside the
+  // interior launch of the same stage (pft_slab_set_boundary_stream)
+  const size_t cnt_bytes = 64 + sizeof(EpsShard) * 2 * PFT_EPS_SHARDS;
   if (e == hipSuccess) e = hipMalloc((void**)&s->pub_count, cnt_bytes);
   if (e == hipSuccess) e = hipMemsetAsync(s->pub_count, 0, cnt_bytes, s->stream);
   if (e == hipSuccess) s->eps_shards = (EpsShard*)((char*)s->pub_count + 64);
@@ -2275,6 +2290,10 @@ int pft_slab_destroy(pft_slab* s)
   if (s->stream) (void)hipStreamDestroy(s->stream);
   if (s->comm) (void)hipStreamDestroy(s->comm);
   if (s->side) (void)hipStreamDestroy(s->side);
+  if (s->bnd) (void)hipStreamDestroy(s->bnd);
+  if (s->ev_bnd) (void)hipEventDestroy(s->ev_bnd);
+  if (s->ev_pre) (void)hipEventDestroy(s->ev_pre);
+  if (s->ev_copy) (void)hipEventDestroy(s->ev_copy);
   if (s->ev_eps) (void)hipEventDestroy(s->ev_eps);
   for (int i = 0; i < 3; ++i)
     if (s->ev_order[i]) (void)hipEventDestroy(s->ev_order[i]);
@@ -2616,7 +2635,7 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   a.out = out;
   a.noise = s->noise;
   a.eps_bits = s->scratch;
-  a.shards = s->eps_shards;
+  a.shards = s->eps_shards + (bnd ? PFT_EPS_SHARDS : 0);
   a.nonfinite = (unsigned int*)(s->scratch + 1);
   a.fs = s->fs;
   a.n1 = s->d.n1;
@@ -2729,12 +2748,21 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
     extra = true;
   }
   if (extra) g.x += 1;
-  const hipStream_t st = s->stream;
+  hipStream_t st = s->stream;
+  if (bnd && s->bnd_mode) {
+    HIPCHK(hipEventRecord(s->ev_pre, s->stream));
+    HIPCHK(hipStreamWaitEvent(s->bnd, s->ev_pre, 0));
+    st = s->bnd;
+  }
   if (gls)
     launch_stage<true>(stage, mode, kind, wx, g, st, a, s->c);
   else
     launch_stage<false>(stage, mode, kind, wx, g, st, a, s->c);
   HIPCHK(hipGetLastError());
+  if (bnd && s->bnd_mode) {
+    HIPCHK(hipEventRecord(s->ev_bnd, s->bnd));
+    s->bnd_pending = 1;
+  }
   return 0;
 }
 
@@ -3315,7 +3343,6 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
   a.out = (first == 2 ? s->buf[PFT_BUF_K3] : s->buf[PFT_BUF_XN]) - s->plane;
   a.noise = s->noise;
   a.eps_bits = s->scratch;
-  a.shards = s->eps_shards;
   a.nonfinite = (unsigned int*)(s->scratch + 1);
   a.fs = s->fs;
   a.n1 = s->d.n1;
@@ -3326,6 +3353,7 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
   a.has_above = s->d.has_above;
   // k_begin == PFT_K_BOUNDARY2: planes 0, 1 and n3-2, n3-1 in one launch (two 2-plane chunks)
   const bool bnd = k_begin == PFT_K_BOUNDARY2;
+  a.shards = s->eps_shards + (bnd ? PFT_EPS_SHARDS : 0);
   if (bnd || k_begin < 0) k_begin = 0;
   if (bnd || k_end < 0 || k_end > s->d.n3) k_end = s->d.n3;
   if (k_end <= k_begin) return 0;
@@ -3377,7 +3405,12 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
     s->pub_slot = j;
   }
   const dim3 g((unsigned)(a.ntile * a.nchunk));
-  const hipStream_t st = s->stream;
+  hipStream_t st = s->stream;
+  if (bnd && s->bnd_mode) {
+    HIPCHK(hipEventRecord(s->ev_pre, s->stream));
+    HIPCHK(hipStreamWaitEvent(s->bnd, s->ev_pre, 0));
+    st = s->bnd;
+  }
   const int lwp = pair_lwp(a.tx);
   if (first == 2) {
     if (glx) launch_pair_mode<2, true>(mode, lwp, g, st, a, s->c);
@@ -3387,6 +3420,10 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
     else launch_pair_mode<4, false>(mode, lwp, g, st, a, s->c);
   }
   HIPCHK(hipGetLastError());
+  if (bnd && s->bnd_mode) {
+    HIPCHK(hipEventRecord(s->ev_bnd, s->bnd));
+    s->bnd_pending = 1;
+  }
   return 0;
 }
 
@@ -3531,6 +3568,8 @@ int pft_slab_ipc_close(pft_slab* s)
     // stream has drained, slab_wait)
     (void)hipStreamSynchronize(s->stream);
     (void)hipStreamSynchronize(s->side);
+    if (s->bnd) (void)hipStreamSynchronize(s->bnd);
+    (void)hipStreamSynchronize(s->comm);
     HIPCHK(hipMemset(s->sig, 0, 2 * sizeof(unsigned long long)));
     HIPCHK(hipDeviceSynchronize());
     s->ipc_poisoned = 0;
@@ -3637,8 +3676,13 @@ int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsign
     for (int i = 0; i < PFT_SEQTAB; ++i) h[i] = s->seq_base + 1 + i;
     HIPCHK(hipMemcpyAsync(s->seqtab, h, sizeof(unsigned long long) * PFT_SEQTAB, hipMemcpyHostToDevice, s->comm));
   }
-  HIPCHK(hipEventRecord(s->ev_order[0], s->stream));
-  HIPCHK(hipStreamWaitEvent(s->comm, s->ev_order[0], 0));
+  // the planes to the neighbour below go on the comm stream, to the one above on the side stream
+  // (two copy engines; ce_streams = 1: all on the comm stream), each followed by its neighbour's flag
+  hipStream_t cs[2] = {s->comm, s->ce_streams == 1 ? s->comm : s->side};
+  hipEvent_t ready = s->bnd_pending ? s->ev_bnd : s->ev_order[0];
+  if (!s->bnd_pending) HIPCHK(hipEventRecord(s->ev_order[0], s->stream));
+  HIPCHK(hipStreamWaitEvent(cs[0], ready, 0));
+  if (cs[1] != cs[0]) HIPCHK(hipStreamWaitEvent(cs[1], ready, 0));
   const int ph = s->phys[role];
   const long P = s->plane, n3 = s->d.n3;
   const long slot = (long)(seq & 1) * 12 * P;
@@ -3653,21 +3697,48 @@ int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsign
         // into its (far -1,) ghost 0 -- contiguous on both ends
         double* dst = side == 0 ? p.base[ph] + q * p.fs + (p.n3 + 1) * P : p.base[ph] + q * p.fs - (deep ? P : 0);
         const double* sp = side == 0 ? src + P : src + (deep ? n3 - 1 : n3) * P;
-        HIPCHK(hipMemcpyAsync(dst, sp, (deep ? 2 : 1) * pb, hipMemcpyDeviceToDeviceNoCU, s->comm));
+        HIPCHK(hipMemcpyAsync(dst, sp, (deep ? 2 : 1) * pb, hipMemcpyDeviceToDeviceNoCU, cs[side]));
       } else {
         // its receive buffer [slot][side][depth][field][plane]: the neighbour below receives our
         // planes as "from above" (side 1), the one above as "from below" (side 0)
         for (int d = 0; d < (deep ? 2 : 1); ++d) {
           double* dst = p.rbuf + slot + ((long)((side == 0 ? 1 : 0) * 2 + d) * 3 + q) * P;
           const double* sp = side == 0 ? src + (1 + d) * P : src + (n3 - d) * P;
-          HIPCHK(hipMemcpyAsync(dst, sp, pb, hipMemcpyDeviceToDeviceNoCU, s->comm));
+          HIPCHK(hipMemcpyAsync(dst, sp, pb, hipMemcpyDeviceToDeviceNoCU, cs[side]));
         }
       }
     }
   }
   const unsigned long long* sv = s->seqtab + (seq - 1 - s->seq_base);
-  if (s->peer[0].on) HIPCHK(hipMemcpyAsync(s->peer[0].sig + 1, sv, 8, hipMemcpyDeviceToDeviceNoCU, s->comm));
-  if (s->peer[1].on) HIPCHK(hipMemcpyAsync(s->peer[1].sig + 0, sv, 8, hipMemcpyDeviceToDeviceNoCU, s->comm));
+  if (cs[1] != cs[0]) {
+    // the table refill above is on the comm stream: the side stream's flag copy follows it
+    HIPCHK(hipEventRecord(s->ev_copy, s->comm));
+    HIPCHK(hipStreamWaitEvent(cs[1], s->ev_copy, 0));
+  }
+  if (s->peer[0].on) HIPCHK(hipMemcpyAsync(s->peer[0].sig + 1, sv, 8, hipMemcpyDeviceToDeviceNoCU, cs[0]));
+  if (s->peer[1].on) HIPCHK(hipMemcpyAsync(s->peer[1].sig + 0, sv, 8, hipMemcpyDeviceToDeviceNoCU, cs[1]));
+  return 0;
+}
+
+int pft_slab_set_boundary_stream(pft_slab* s, int on)
+{
+  if (on && !s->bnd) {
+    int lo = 0, hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIPCHK(hipStreamCreateWithPriority(&s->bnd, hipStreamNonBlocking, hi));
+    HIPCHK(hipEventCreateWithFlags(&s->ev_bnd, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&s->ev_pre, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
+  }
+  if (on && !s->ev_copy) HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
+  // env overrides for A/B: PFT_CE_BND=0 keeps the boundary launch on the compute stream, before
+  // the interior one; PFT_CE_STREAMS=1 puts every copy on the comm stream
+  const char* eb = getenv("PFT_CE_BND");
+  const char* es = getenv("PFT_CE_STREAMS");
+  s->bnd_mode = on && !(eb && atoi(eb) == 0) ? 1 : 0;
+  s->ce_streams = es ? atoi(es) : 2;
+  if (s->ce_streams == 2 && !s->ev_copy) HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
+  s->bnd_pending = 0;
   return 0;
 }
 
@@ -3688,6 +3759,11 @@ int pft_slab_halo_wait(pft_slab* s, unsigned long long seq)
 {
   // flags [0] (from below) and [1] (from above): the stream goes on once both planes are in
   if (s->ipc_poisoned) return slab_poisoned(s, "pft_slab_halo_wait");
+  if (s->bnd_pending) {
+    // the boundary launch ran beside the interior one: its planes are the next launch's input
+    HIPCHK(hipStreamWaitEvent(s->stream, s->ev_bnd, 0));
+    s->bnd_pending = 0;
+  }
   int sides = 0;
   for (int side = 0; side < 2; ++side) {
     if (!s->peer[side].on) continue;
