@@ -1890,6 +1890,47 @@ __global__ __launch_bounds__(256) void halo_recv_kernel(RecvArgs a)
   }
 }
 
+// The receiving side of an exchange in ONE launch (pft_slab_halo_wait): thread 0 of every workgroup
+// waits until both flag words reach seq (system-scope atomic loads of uncached memory: never served
+// from a cache), then -- staged receive -- the workgroups copy the receive buffer into the ghost
+// planes (halo_recv_kernel's loop).  It replaces hipStreamWaitValue64 per flag (the runtime runs each
+// as a kernel of its own, ~3 us apiece) and the separate receive launch.  Every wave exits: the
+// flags come from the neighbours, or from the slab itself when a wait times out (slab_timed_out
+// releases them past every sequence number).
+struct WaitArgs {
+  const unsigned long long* f0;   // flag from below, or null
+  const unsigned long long* f1;   // flag from above, or null
+  unsigned long long seq;
+  int recv;                       // 1: then copy r
+  RecvArgs r;
+};
+
+__global__ __launch_bounds__(256) void halo_wait_kernel(WaitArgs a)
+{
+  if (threadIdx.x == 0) {
+    if (a.f0)
+      while (__hip_atomic_load(a.f0, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.seq) __builtin_amdgcn_s_sleep(2);
+    if (a.f1)
+      while (__hip_atomic_load(a.f1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.seq) __builtin_amdgcn_s_sleep(2);
+  }
+  __syncthreads();
+  if (!a.recv) return;
+  const RecvArgs& r = a.r;
+  const long n = (long)r.nf * r.plane;
+  const long tot = 4L * n;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < tot; e += (long)gridDim.x * blockDim.x) {
+    const int part = (int)(e / n);
+    const int side = part >> 1, depth = part & 1;
+    if (!((r.sides >> side) & 1) || depth >= r.depth) continue;
+    const long rr = e - part * n;
+    const int f = (int)(rr / r.plane);
+    const long c = rr - (long)f * r.plane;
+    const int q = r.f0 + f;
+    const long pl = side == 0 ? (depth == 0 ? 0L : -1L) : (long)r.n3 + 1 + depth;
+    r.dst[q * r.fs + pl * r.plane + c] = r.rbuf[((long)(side * 2 + depth) * 3 + q) * r.plane + c];
+  }
+}
+
 // raises the neighbours' flags once the kernels before it on the stream (the put, or a stage
 // kernel that stored its boundary planes into the neighbours' ghost planes) have completed: their
 // stores are released at kernel end; with a neighbour on another GPU a system-scope fence first
@@ -1954,6 +1995,7 @@ struct pft_slab {
   // the compute stream instead of before it; the exchange waits for ev_bnd, and so does the compute
   // stream before the next launch (pft_slab_halo_wait)
   int bnd_mode, bnd_pending, ce_streams;
+  int wait_streamops;    // A/B: halo waits as hipStreamWaitValue64 (env PFT_WAIT_STREAMOPS=1)
   hipStream_t bnd;
   hipEvent_t ev_bnd, ev_pre, ev_copy;
   int put_role, put_f0, put_f1, put_deep;   // the exchange the last halo_put2 sent (its wait receives it)
@@ -2204,6 +2246,8 @@ int pft_slab_create(pft_slab** out, const pft_slab_desc* d, const pft_consts* c)
     s->pair_ntile = pair_geometry(d->n1, d->n2, &s->pair_tx, &s->pair_ty);
     const char* eg = getenv("PFT_GATE_FLIP");
     s->gate_flip = eg ? atoi(eg) : 0;
+    const char* ew = getenv("PFT_WAIT_STREAMOPS");
+    s->wait_streamops = ew ? atoi(ew) : 0;
     const char* et = getenv("PFT_IPC_TIMEOUT");
     s->timeout_s = (et && atof(et) > 0.0) ? atof(et) : 300.0;
   }
@@ -3731,11 +3775,13 @@ int pft_slab_set_boundary_stream(pft_slab* s, int on)
     HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
   }
   if (on && !s->ev_copy) HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
-  // env overrides for A/B: PFT_CE_BND=0 keeps the boundary launch on the compute stream, before
-  // the interior one; PFT_CE_STREAMS=1 puts every copy on the comm stream
+  // env overrides for A/B: PFT_CE_BND=1 runs the boundary launch on its own stream beside the
+  // interior one (measured slower: its workgroups are dispatched interleaved with the interior's
+  // and it ends late, profiles/r05_ce_trace_*.txt); PFT_CE_STREAMS=1 puts every copy on the comm
+  // stream
   const char* eb = getenv("PFT_CE_BND");
   const char* es = getenv("PFT_CE_STREAMS");
-  s->bnd_mode = on && !(eb && atoi(eb) == 0) ? 1 : 0;
+  s->bnd_mode = on && eb && atoi(eb) == 1 ? 1 : 0;
   s->ce_streams = es ? atoi(es) : 2;
   if (s->ce_streams == 2 && !s->ev_copy) HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
   s->bnd_pending = 0;
@@ -3765,15 +3811,20 @@ int pft_slab_halo_wait(pft_slab* s, unsigned long long seq)
     s->bnd_pending = 0;
   }
   int sides = 0;
+  WaitArgs w;
+  memset(&w, 0, sizeof(w));
+  w.seq = seq;
   for (int side = 0; side < 2; ++side) {
     if (!s->peer[side].on) continue;
-    HIPCHK(hipStreamWaitValue64(s->stream, s->sig + side, seq, hipStreamWaitValueGte, ~0ULL));
+    (side == 0 ? w.f0 : w.f1) = s->sig + side;
     if (s->peer[side].staged) sides |= 1 << side;
   }
+  if (!w.f0 && !w.f1) return 0;
+  int blocks = 1;
   if (sides) {
     // staged: what the neighbours put into the receive buffer, into the ghost planes of the
     // exchange's buffer (the one the last halo_put2 sent: every rank runs the same sequence)
-    RecvArgs r;
+    RecvArgs& r = w.r;
     r.rbuf = s->rbuf + (long)(seq & 1) * 12 * s->plane;
     r.dst = s->buf[s->put_role];
     r.fs = s->fs;
@@ -3783,11 +3834,19 @@ int pft_slab_halo_wait(pft_slab* s, unsigned long long seq)
     r.nf = s->put_f1 - s->put_f0;
     r.depth = s->put_deep ? 2 : 1;
     r.sides = sides;
+    w.recv = 1;
     const long n = 4L * r.nf * s->plane;
-    const int blocks = (int)std::min<long>(1024, std::max<long>(1, (n + 255) / 256));
-    halo_recv_kernel<<<blocks, 256, 0, s->stream>>>(r);
-    HIPCHK(hipGetLastError());
+    blocks = (int)std::min<long>(1024, std::max<long>(1, (n + 255) / 256));
   }
+  if (s->wait_streamops) {
+    // A/B (PFT_WAIT_STREAMOPS=1): the runtime's stream waits, then a separate receive launch
+    for (int side = 0; side < 2; ++side)
+      if (s->peer[side].on) HIPCHK(hipStreamWaitValue64(s->stream, s->sig + side, seq, hipStreamWaitValueGte, ~0ULL));
+    if (sides) halo_recv_kernel<<<blocks, 256, 0, s->stream>>>(w.r);
+  } else {
+    halo_wait_kernel<<<blocks, 256, 0, s->stream>>>(w);
+  }
+  HIPCHK(hipGetLastError());
   return 0;
 }
 
