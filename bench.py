@@ -97,9 +97,10 @@ def parse():
     ap.add_argument("--transport", choices=("auto", "ipc", "ipc-ce", "rccl"), default="auto",
                     help="N>1 (and --self-exchange) inter-slab transport (pft_comm.h): ipc = IPC-mapped "
                          "neighbour slabs, boundary planes stored into their ghost planes + flag words; "
-                         "rccl = ncclSend/ncclRecv on a priority stream beside the interior sweep; auto "
-                         "(default) = rccl with one GPU per rank, ipc when ranks share a GPU (RCCL refuses "
-                         "that) and for --self-exchange (DESIGN section 6)")
+                         "ipc-ce = the same planes and flags as copy-engine (SDMA) copies beside the interior "
+                         "launch; rccl = ncclSend/ncclRecv on a priority stream beside the interior sweep; "
+                         "auto (default) = ipc-ce with one GPU per rank, ipc when ranks share a GPU and for "
+                         "--self-exchange (DESIGN section 6)")
     ap.add_argument("--self-exchange", action="store_true",
                     help="diagnostic, 1 GPU: run the N>1 path of --transport (ipc: put kernel + flag waits "
                          "per stage; rccl: boundary planes first, halo exchange beside the interior sweep, "
@@ -140,7 +141,11 @@ def main():
         sys.exit("no HIP device visible (the benchmark has no CPU fallback)")
     dev = local % ndev           # one process per GPU; more ranks than GPUs share round-robin
     if a.transport == "auto":
-        a.transport = "ipc" if (world > ndev or a.self_exchange) else "rccl"
+        # one GPU per rank: the exchange on the copy engines beside the interior launch (the planes
+        # cross xGMI without CUs; RCCL's kernel waits for the launch that holds every CU, and the
+        # put kernel would run after it); ranks sharing a GPU, and the self exchange: the put kernel
+        # (a local copy, the cheapest there).  DESIGN.md section 6.
+        a.transport = "ipc" if (world > ndev or a.self_exchange) else "ipc-ce"
     dist = None
     comm = None
     if world > 1:
