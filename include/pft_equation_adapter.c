@@ -27,6 +27,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 #include "pft_model.h"
 #include "pft_solver.h"
 #include "pft_comm.h"
@@ -72,6 +73,23 @@ static int pft_adapter_comm_init(void)
 	if(!ok) {
 		fprintf(stderr, "pft_adapter: rank %d: no HIP device on %s rank\n", MPIrank, ndev >= 1 ? "another" : "this");
 		return 1;
+	}
+	{
+		/* PFT_ADAPTER_TRANSPORT=ipc-ce (or ipc): every rank on ONE node, the exchange over IPC-mapped
+		   slabs -- on the copy engines beside the interior launch with ipc-ce;
+		   the shared-memory name comes from the master.  Default: RCCL, which also spans nodes. */
+		const char * tr = getenv("PFT_ADAPTER_TRANSPORT");
+		if(tr && (strcmp(tr, "ipc-ce") == 0 || strcmp(tr, "ipc") == 0)) {
+			char name[64];
+			int rc;
+			memset(name, 0, sizeof(name));
+			if(MPIrank == 0) snprintf(name, sizeof(name), "/pft_adapter_%ld", (long)getpid());
+			MPI_Bcast(name, (int)sizeof(name), MPI_CHAR, MPIrankmap[0], MPI_COMM_WORLD);
+			rc = pft_comm_init_ipc(&pft_adapter_comm, MPIprocs, MPIrank, name, MPIrank % ndev);
+			if(!rc && strcmp(tr, "ipc-ce") == 0) rc = pft_comm_set_copy_engine(pft_adapter_comm, 1);
+			if(rc) return 1;
+			return pft_comm_set_current(pft_adapter_comm) ? 1 : 0;
+		}
 	}
 	/* one process per GPU, ranks packed per node */
 	if(pft_comm_init_rccl(&pft_adapter_comm, MPIprocs, MPIrank, msg + 1, MPIrank % ndev)) return 1;
