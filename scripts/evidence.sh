@@ -53,7 +53,7 @@ timeout -k 10 300 python bench.py --steps 200 --no-cpu --host-boundary > $O/benc
 for dom in "400 0.06,0.06,0.015 n8" "318 0.06,0.06,0.03 n4" "252 0.06,0.06,0.06 n2"; do
   set -- $dom
   timeout -k 10 300 python bench.py --steps 100 --no-cpu --grid-nodes $1 --domain $2 > $O/bench_slab_$3.json 2>> $O/bench_var.err; fatal $? slab_$3
-  for tr in ipc rccl; do
+  for tr in ipc ipc-ce rccl; do
     timeout -k 10 300 python bench.py --steps 100 --no-cpu --grid-nodes $1 --domain $2 --self-exchange --transport $tr > $O/bench_slab_$3_selfx_$tr.json 2>> $O/bench_var.err; fatal $? slab_$3_selfx_$tr
   done
 done
@@ -65,4 +65,5 @@ done
 timeout -k 10 300 rocprofv3 --kernel-trace -d $O/prof/driver -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu > $O/prof/driver_bench.json 2> $O/prof/driver.err; fatal $? driver_trace
 # bench.py --gpus N rehearsed on this one GPU (ipc ranks) with its decomposition parity check
 bash scripts/bench_multi.sh > $O/bench_multi.log 2>&1; fatal $? bench_multi
+TRANSPORT=ipc-ce TAG=_ce bash scripts/bench_multi.sh > $O/bench_multi_ce.log 2>&1; fatal $? bench_multi_ce
 echo done >> $O/status.log
