@@ -283,6 +283,10 @@ int pft_slab_halo_put2(pft_slab * s, int role, int f0, int f1, int deep, unsigne
    (8-byte copies), no kernel -- beside the interior launch that follows on the compute stream.
    The receiver's side is pft_slab_halo_wait as for halo_put2. */
 int pft_slab_halo_put_ce(pft_slab * s, int role, int f0, int f1, int deep, unsigned long long seq);
+/* marks the point of the compute stream the next put_ce sends from (an event after the boundary
+   launch), so that the host can enqueue the interior launch before the copies: put_ce then waits
+   for the mark instead of recording one */
+int pft_slab_halo_mark(pft_slab * s);
 /* 1: a launch of the boundary planes (k_begin PFT_K_BOUNDARY / PFT_K_BOUNDARY2) runs on a stream of
    its own at the greatest priority, beside the interior launch that follows on the compute stream,
    instead of before it; the copy-engine exchange starts when it ends, and pft_slab_halo_wait makes

@@ -81,6 +81,7 @@ struct pft_comm {
   unsigned long long hseq;   // host collective rounds so far (identical on every rank)
   unsigned long long dseq;   // device halo exchanges so far (identical on every rank)
   double timeout_s;
+  int ce_buf, ce_f0, ce_f1, ce_deep;   // the copy-engine exchange marked by halo_start
   int ce;                    // ipc: the halo planes go on the copy engines beside the interior launch
                              // (pft_comm_set_copy_engine; env PFT_IPC_CE)
   void* bcast_pinned;        // rccl: pinned host staging of pft_comm_bcast
@@ -524,10 +525,18 @@ static int halo_start(pft_comm* c, int buf, int f0, int f1, bool deep = false)
   if (c->kind == KIND_IPC) {
     const unsigned long long seq = ++c->dseq;
     if (c->ce) {
-      // copy engines: the planes and the flags go out on the comm stream, beside whatever the
-      // compute stream runs next (the interior launch); halo_finish waits for our own flags
-      int rc = pft_slab_halo_put_ce(s, buf, f0, f1, deep ? 1 : 0, seq);
-      if (!rc) c->pending = 1;
+      // copy engines: mark the compute stream here (after the boundary launch); halo_finish, which
+      // the caller reaches after enqueueing the interior launch, enqueues the planes and flags on
+      // the copy streams (they start at the mark, beside the interior launch) and then the wait for
+      // our own flags -- the interior launch is not held behind the host's copy calls
+      int rc = pft_slab_halo_mark(s);
+      if (!rc) {
+        c->pending = 1;
+        c->ce_buf = buf;
+        c->ce_f0 = f0;
+        c->ce_f1 = f1;
+        c->ce_deep = deep ? 1 : 0;
+      }
       return rc;
     }
     // stream-ordered on the compute stream: put (boundary planes into the neighbours' ghost
@@ -603,7 +612,10 @@ int pft_comm_halo_finish(pft_comm* c)
 {
   if (!pft_comm_splits(c) || !c->pending) return 0;
   c->pending = 0;
-  if (c->kind == KIND_IPC) return pft_slab_halo_wait(c->slab, c->dseq);
+  if (c->kind == KIND_IPC) {
+    int rc = pft_slab_halo_put_ce(c->slab, c->ce_buf, c->ce_f0, c->ce_f1, c->ce_deep, c->dseq);
+    return rc ? rc : pft_slab_halo_wait(c->slab, c->dseq);
+  }
   HCHK(hipStreamWaitEvent((hipStream_t)pft_slab_stream(c->slab), c->ev_done, 0));
   return 0;
 }

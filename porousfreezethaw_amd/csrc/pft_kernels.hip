@@ -1995,6 +1995,7 @@ struct pft_slab {
   // the compute stream instead of before it; the exchange waits for ev_bnd, and so does the compute
   // stream before the next launch (pft_slab_halo_wait)
   int bnd_mode, bnd_pending, ce_streams;
+  int ce_marked;         // pft_slab_halo_mark recorded ev_order[0] after the launch the next put_ce sends
   int wait_streamops;    // A/B: halo waits as hipStreamWaitValue64 (env PFT_WAIT_STREAMOPS=1)
   hipStream_t bnd;
   hipEvent_t ev_bnd, ev_pre, ev_copy;
@@ -3700,6 +3701,8 @@ int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsign
 {
   if (role < 0 || role >= PFT_BUF_COUNT || f0 < 0 || f1 > 3 || f1 <= f0 || seq == 0) return -2;
   if (s->ipc_poisoned) return slab_poisoned(s, "pft_slab_halo_put_ce");
+  const int marked = s->ce_marked;
+  s->ce_marked = 0;
   s->put_role = role;
   s->put_f0 = f0;
   s->put_f1 = f1;
@@ -3724,7 +3727,7 @@ int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsign
   // (two copy engines; ce_streams = 1: all on the comm stream), each followed by its neighbour's flag
   hipStream_t cs[2] = {s->comm, s->ce_streams == 1 ? s->comm : s->side};
   hipEvent_t ready = s->bnd_pending ? s->ev_bnd : s->ev_order[0];
-  if (!s->bnd_pending) HIPCHK(hipEventRecord(s->ev_order[0], s->stream));
+  if (!s->bnd_pending && !marked) HIPCHK(hipEventRecord(s->ev_order[0], s->stream));
   HIPCHK(hipStreamWaitEvent(cs[0], ready, 0));
   if (cs[1] != cs[0]) HIPCHK(hipStreamWaitEvent(cs[1], ready, 0));
   const int ph = s->phys[role];
@@ -3761,6 +3764,14 @@ int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsign
   }
   if (s->peer[0].on) HIPCHK(hipMemcpyAsync(s->peer[0].sig + 1, sv, 8, hipMemcpyDeviceToDeviceNoCU, cs[0]));
   if (s->peer[1].on) HIPCHK(hipMemcpyAsync(s->peer[1].sig + 0, sv, 8, hipMemcpyDeviceToDeviceNoCU, cs[1]));
+  return 0;
+}
+
+int pft_slab_halo_mark(pft_slab* s)
+{
+  if (s->ipc_poisoned) return slab_poisoned(s, "pft_slab_halo_mark");
+  if (!s->bnd_pending) HIPCHK(hipEventRecord(s->ev_order[0], s->stream));
+  s->ce_marked = 1;
   return 0;
 }
 
