@@ -140,6 +140,7 @@ def main():
     if ndev < 1:
         sys.exit("no HIP device visible (the benchmark has no CPU fallback)")
     dev = local % ndev           # one process per GPU; more ranks than GPUs share round-robin
+    transport_auto = a.transport == "auto"
     if a.transport == "auto":
         # one GPU per rank: the exchange on the copy engines beside the interior launch (the planes
         # cross xGMI without CUs; RCCL's kernel waits for the launch that holds every CU, and the
@@ -172,10 +173,42 @@ def main():
     prm = P.params_array(base)
     beads = np.load(os.path.join(REPO, "tests", "golden", "beads.npy"))
     t0 = time.time()
-    sim = P.Simulation(n1, n2, total_n3, Ls, a.mode, prm, nprocs=world, rank=rank, beads=beads,
-                       tau=base["tau"], tau_min=base["tau_min"], delta=base["delta"],
-                       gl_static=a.gl_static, kz=a.kz or None, tile=a.tile,
-                       recompute=not a.no_recompute, device_ic=not a.host_ic)
+
+    def make_sim():
+        return P.Simulation(n1, n2, total_n3, Ls, a.mode, prm, nprocs=world, rank=rank, beads=beads,
+                            tau=base["tau"], tau_min=base["tau_min"], delta=base["delta"],
+                            gl_static=a.gl_static, kz=a.kz or None, tile=a.tile,
+                            recompute=not a.no_recompute, device_ic=not a.host_ic)
+
+    if world > 1:
+        # The first exchanges (the device IC's ghost planes) run inside the setup.  If the ipc transport
+        # the run chose by itself fails there on any rank (mapping a neighbour's buffers across GPUs,
+        # say: the attach agrees its outcome across ranks, so all fail together), every rank falls
+        # back to RCCL rather than ending without a measurement; the JSON line names the transport.
+        sim, fail = None, 0
+        try:
+            sim = make_sim()
+        except Exception as e:  # noqa: BLE001
+            print(f"rank {rank}: setup over {a.transport} failed: {e}", file=sys.stderr)
+            fail = 1
+        import torch
+        ft = torch.tensor([fail], dtype=torch.int64)
+        dist.all_reduce(ft, op=dist.ReduceOp.MAX)
+        if int(ft.item()):
+            if not (transport_auto and a.transport in ("ipc", "ipc-ce")):
+                sys.exit(f"rank {rank}: setup over {a.transport} failed on a rank")
+            if sim is not None:
+                sim.close()
+            else:
+                L.RK_MPI_SA_cleanup()
+                L.FreePrecalcData()
+            L.pft_comm_set_current(None)
+            L.pft_comm_destroy(comm)
+            print(f"rank {rank}: every rank falls back to RCCL", file=sys.stderr)
+            comm, a.transport = make_comm(L, "rccl", world, rank, dev, dist, fallback=False)
+            sim = make_sim()
+    else:
+        sim = make_sim()
     init_s = time.time() - t0
     cells_rank = n1 * n2 * sim.grid.n3
     cells_total = n1 * n2 * total_n3

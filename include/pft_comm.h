@@ -81,6 +81,9 @@ pft_comm * pft_comm_current(void);
 
 /* attach the slab whose buffers are exchanged */
 int pft_comm_attach(pft_comm * c, pft_slab * s);
+/* ipc: a rank could not export or map a neighbour's buffers; every rank's attach returns it (or
+   its own error) in the same round */
+#define PFT_ERR_IPC_ATTACH (-5004)
 
 /* exchange the boundary planes of buffer `buf` (fields [f0, f1)) with the z-neighbours.
    halo_start: ordered after the work already on the slab's compute stream, runs on the slab's

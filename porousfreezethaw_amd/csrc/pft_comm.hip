@@ -466,29 +466,38 @@ static int ipc_attach(pft_comm* c, pft_slab* s)
     c->slab = nullptr;
   }
   if (!s) return 0;
+  // both rounds carry each rank's local outcome (iv), so that a rank that cannot export or map a
+  // neighbour's buffers makes every rank fail here at once -- none is left waiting in a later round
+  // until PFT_IPC_TIMEOUT
   IpcSlot* me = &c->shm->slot[c->rank];
-  if ((rc = pft_slab_ipc_export(s, me->handles))) return rc;
+  int lrc = pft_slab_ipc_export(s, me->handles);
   me->n3 = pft_slab_nz(s);
   me->device = c->device;
   me->fs = (long)pft_slab_field_stride(s);
   me->staged = pft_ipc_staged_env();
-  if ((rc = ipc_round(c, nullptr, 0, nullptr, 0, &recs))) return rc;   // every slot is published
+  if ((rc = ipc_round(c, nullptr, lrc ? 1 : 0, nullptr, 0, &recs))) return rc;   // every slot is published
+  for (int q = 0; q < c->size; ++q)
+    if (recs[q].iv) return lrc ? lrc : PFT_ERR_IPC_ATTACH;
   if (c->self_x) {
-    if ((rc = pft_slab_ipc_set_peer(s, 0, nullptr, 0, 0, 0, 0)) || (rc = pft_slab_ipc_set_peer(s, 1, nullptr, 0, 0, 0, 0)))
-      return rc;
+    if (!(lrc = pft_slab_ipc_set_peer(s, 0, nullptr, 0, 0, 0, 0))) lrc = pft_slab_ipc_set_peer(s, 1, nullptr, 0, 0, 0, 0);
   } else {
     if (c->rank > 0) {
       const IpcSlot* b = &c->shm->slot[c->rank - 1];
-      if ((rc = pft_slab_ipc_set_peer(s, 0, b->handles, b->n3, b->fs, b->device, b->staged))) return rc;
+      lrc = pft_slab_ipc_set_peer(s, 0, b->handles, b->n3, b->fs, b->device, b->staged);
     }
-    if (c->rank < c->size - 1) {
+    if (!lrc && c->rank < c->size - 1) {
       const IpcSlot* a = &c->shm->slot[c->rank + 1];
-      if ((rc = pft_slab_ipc_set_peer(s, 1, a->handles, a->n3, a->fs, a->device, a->staged))) return rc;
+      lrc = pft_slab_ipc_set_peer(s, 1, a->handles, a->n3, a->fs, a->device, a->staged);
     }
   }
+  if (!lrc) lrc = pft_slab_set_boundary_stream(s, c->ce);
   // the slots are reused by the next attach only after everyone has read them
-  if ((rc = ipc_round(c, nullptr, 0, nullptr, 0, &recs))) return rc;
-  if ((rc = pft_slab_set_boundary_stream(s, c->ce))) return rc;
+  if ((rc = ipc_round(c, nullptr, lrc ? 1 : 0, nullptr, 0, &recs))) return rc;
+  for (int q = 0; q < c->size; ++q)
+    if (recs[q].iv) {
+      pft_slab_ipc_close(s);
+      return lrc ? lrc : PFT_ERR_IPC_ATTACH;
+    }
   c->slab = s;
   return 0;
 }

@@ -224,7 +224,7 @@ static int ensure_slab(void)
 		R.slab_grid = g; R.slab_gls = R.opt_gls; R.slab_dev = R.opt_dev;
 		R.device_valid = 0;
 	}
-	pft_comm_attach(comm(), R.slab);
+	if((rc = pft_comm_attach(comm(), R.slab))) return rc;
 	return pft_slab_set_noise(R.slab, pft_model_noise());
 }
 
