@@ -491,6 +491,11 @@ static int ipc_attach(pft_comm* c, pft_slab* s)
     }
   }
   if (!lrc) lrc = pft_slab_set_boundary_stream(s, c->ce);
+  {
+    // fault injection (tests/test_ipc_multiprocess.py): this rank fails to map its neighbours
+    const char* ef = getenv("PFT_IPC_FAIL_ATTACH");
+    if (!lrc && ef && atoi(ef) == 1) lrc = PFT_ERR_IPC_ATTACH;
+  }
   // the slots are reused by the next attach only after everyone has read them
   if ((rc = ipc_round(c, nullptr, lrc ? 1 : 0, nullptr, 0, &recs))) return rc;
   for (int q = 0; q < c->size; ++q)

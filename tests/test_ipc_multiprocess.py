@@ -295,3 +295,15 @@ def test_lost_copy_engine_halo_ends_in_device_error(tmp_path):
         assert int(r["status"]) in (-5000, -5002)
         assert float(r["seconds"]) < 60
         assert int(r["rc2"]) == P.PFT_SOLVE_DEVICE_ERROR
+
+
+def test_failed_attach_fails_every_rank_at_once(tmp_path):
+    """rank 1 cannot map its neighbour's buffers (fault injection PFT_IPC_FAIL_ATTACH=1): the attach
+    agrees its outcome across ranks, so both ranks' first solve returns PFT_SOLVE_DEVICE_ERROR at
+    once -- rank 0 is not left in the attach's second round until PFT_IPC_TIMEOUT (here 120 s)"""
+    res = _run_ranks(tmp_path, 2, timeout=240, case="g20", times=[36.0], raw_rc=True,
+                     rank_env={1: {"PFT_IPC_FAIL_ATTACH": "1"}, 0: {"PFT_IPC_CE": "1"}})
+    for r in res:
+        assert int(r["rc"]) == P.PFT_SOLVE_DEVICE_ERROR
+        assert float(r["seconds"]) < 30
+    assert int(res[1]["status"]) == -5004 and int(res[0]["status"]) == -5004
