@@ -1081,9 +1081,10 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
 // The row pitch LWP (pairs) is a template parameter, a compile-time constant so that every LDS
 // access is a per-lane base + an immediate offset: 22 (tiles up to 40 cells wide, 19 rows) or 12
 // (up to 20 cells wide, 38 rows: n1 = 100 in 5 tiles of 20 where 40-wide tiles leave a sixth idle)
-#ifndef PFT_PAIR_MIN_CELLS_PER_CU
-#define PFT_PAIR_MIN_CELLS_PER_CU 4096
-#endif
+// measured crossover (profiles/r05_pair_threshold.txt, stage launches against pair kernels forced):
+// 128^3 (2048 cells per CU) -10%, 136^3 (2456) -1.4%, 144^3 (2916) +16%, 152^3 (3429) +18%, 160^3
+// (4000) +9%, 200^3 (7.8 Ki) +7-9%
+#define PFT_PAIR_MIN_CELLS_PER_CU 2560
 
 struct PairArgs {
   const double* x;
