@@ -188,6 +188,11 @@ def main():
         sim, fail = None, 0
         try:
             sim = make_sim()
+            # the setup's exchange delivered the neighbours' boundary planes bit for bit (a transport
+            # that maps but does not deliver -- across GPUs, say -- is caught here, not at the parity
+            # check after the timed region)
+            if not a.host_ic and not halo_delivered(L, sim, dist, world, rank):
+                raise RuntimeError("the ghost planes after the setup exchange differ from the neighbours' planes")
         except Exception as e:  # noqa: BLE001
             print(f"rank {rank}: setup over {a.transport} failed: {e}", file=sys.stderr)
             fail = 1
@@ -430,6 +435,48 @@ def main():
         dist.destroy_process_group()
     if not ok:
         sys.exit(f"parity: the {world}-slab run differs from the single-slab run of the same steps")
+
+
+def halo_delivered(L, sim, dist, world, rank):
+    """after the setup (the IC and its one-plane exchange of X), every rank's ghost planes hold its
+    z-neighbours' boundary planes bit for bit (u, p, gl of X).  Collective over gloo; every rank gets
+    the same answer."""
+    import torch
+    L.pft_solver_slab.restype = C.c_void_p
+    L.pft_slab_buffer.restype = C.c_void_p
+    L.pft_slab_buffer.argtypes = [C.c_void_p, C.c_int]
+    L.pft_slab_plane.restype = C.c_size_t
+    L.pft_slab_plane.argtypes = [C.c_void_p]
+    L.pft_slab_field_stride.restype = C.c_size_t
+    L.pft_slab_field_stride.argtypes = [C.c_void_p]
+    L.pft_slab_nz.argtypes = [C.c_void_p]
+    L.pft_flat_d2h.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+    L.pft_stream_sync.argtypes = [C.c_void_p]
+    slab = L.pft_solver_slab()
+    ok = 1
+    planes = {}
+    try:
+        L.pft_hip_device_sync()
+        base, P_, fs, n3 = L.pft_slab_buffer(slab, 0), L.pft_slab_plane(slab), L.pft_slab_field_stride(slab), L.pft_slab_nz(slab)
+        for name, k in (("g0", 0), ("b1", 1), ("bn", n3), ("gn", n3 + 1)):
+            a = np.empty((3, P_))
+            for q in range(3):
+                if L.pft_flat_d2h(a[q].ctypes.data, base + 8 * (q * fs + k * P_), P_, None):
+                    ok = 0
+            planes[name] = a
+        L.pft_stream_sync(None)
+    except Exception:  # noqa: BLE001
+        ok = 0
+    rec = {"ok": ok, "sha": {k: hashlib.sha256(v.tobytes()).hexdigest() for k, v in planes.items()}}
+    allrec = [None] * world
+    dist.all_gather_object(allrec, rec)
+    good = all(r["ok"] for r in allrec)
+    for r in range(world):
+        if r > 0 and good:
+            good = allrec[r]["sha"]["g0"] == allrec[r - 1]["sha"]["bn"]
+        if r < world - 1 and good:
+            good = allrec[r]["sha"]["gn"] == allrec[r + 1]["sha"]["b1"]
+    return good
 
 
 def slab_digest(sim):
