@@ -1990,7 +1990,7 @@ struct pft_slab {
   unsigned long long* seqtab;
   unsigned long long* seqhost;
   unsigned long long seq_base;
-  int seq_half;
+  int seq_half, seq_n;
   // boundary launches on their own stream (pft_slab_set_boundary_stream; the copy-engine exchange):
   // a launch of the boundary planes (PFT_K_BOUNDARY/2) runs on `bnd` beside the interior launch on
   // the compute stream instead of before it; the exchange waits for ev_bnd, and so does the compute
@@ -1999,7 +1999,7 @@ struct pft_slab {
   int ce_marked;         // pft_slab_halo_mark recorded ev_order[0] after the launch the next put_ce sends
   int wait_streamops;    // A/B: halo waits as hipStreamWaitValue64 (env PFT_WAIT_STREAMOPS=1)
   hipStream_t bnd;
-  hipEvent_t ev_bnd, ev_pre, ev_copy;
+  hipEvent_t ev_bnd, ev_pre, ev_copy, ev_side;
   int put_role, put_f0, put_f1, put_deep;   // the exchange the last halo_put2 sent (its wait receives it)
   SlabPeer peer[2];              // [0] the neighbour below, [1] above
   int drop_puts;                 // fault injection: halo puts and flag raises skipped (PFT_IPC_DROP_PUTS)
@@ -2340,6 +2340,7 @@ int pft_slab_destroy(pft_slab* s)
   if (s->ev_bnd) (void)hipEventDestroy(s->ev_bnd);
   if (s->ev_pre) (void)hipEventDestroy(s->ev_pre);
   if (s->ev_copy) (void)hipEventDestroy(s->ev_copy);
+  if (s->ev_side) (void)hipEventDestroy(s->ev_side);
   if (s->ev_eps) (void)hipEventDestroy(s->ev_eps);
   for (int i = 0; i < 3; ++i)
     if (s->ev_order[i]) (void)hipEventDestroy(s->ev_order[i]);
@@ -3714,15 +3715,24 @@ int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsign
     HIPCHK(hipMalloc((void**)&s->seqtab, sizeof(unsigned long long) * PFT_SEQTAB));
     HIPCHK(hipHostMalloc((void**)&s->seqhost, 2 * sizeof(unsigned long long) * PFT_SEQTAB, hipHostMallocDefault));
     s->seq_base = ~0ULL;
+    // test hook PFT_CE_SEQTAB=n (2..4096): a table of n numbers, refilled every n exchanges
+    const char* et = getenv("PFT_CE_SEQTAB");
+    s->seq_n = (et && atoi(et) >= 2 && atoi(et) <= PFT_SEQTAB) ? atoi(et) : PFT_SEQTAB;
   }
-  if (s->seq_base == ~0ULL || seq <= s->seq_base || seq > s->seq_base + PFT_SEQTAB) {
+  const int NSEQ = s->seq_n;
+  if (s->seq_base == ~0ULL || seq <= s->seq_base || seq > s->seq_base + NSEQ) {
     // the next block of sequence numbers, from the pinned half not used by the previous refill
     // (that one's copy is PFT_SEQTAB exchanges old: complete)
-    s->seq_base = (seq - 1) / PFT_SEQTAB * PFT_SEQTAB;
+    s->seq_base = (seq - 1) / NSEQ * NSEQ;
     s->seq_half ^= 1;
+    if (s->ce_streams != 1) {
+      // the side stream's last flag copy reads the old table: the refill (comm stream) waits for it
+      HIPCHK(hipEventRecord(s->ev_side, s->side));
+      HIPCHK(hipStreamWaitEvent(s->comm, s->ev_side, 0));
+    }
     unsigned long long* h = s->seqhost + (size_t)s->seq_half * PFT_SEQTAB;
-    for (int i = 0; i < PFT_SEQTAB; ++i) h[i] = s->seq_base + 1 + i;
-    HIPCHK(hipMemcpyAsync(s->seqtab, h, sizeof(unsigned long long) * PFT_SEQTAB, hipMemcpyHostToDevice, s->comm));
+    for (int i = 0; i < NSEQ; ++i) h[i] = s->seq_base + 1 + i;
+    HIPCHK(hipMemcpyAsync(s->seqtab, h, sizeof(unsigned long long) * NSEQ, hipMemcpyHostToDevice, s->comm));
   }
   // the planes to the neighbour below go on the comm stream, to the one above on the side stream
   // (two copy engines; ce_streams = 1: all on the comm stream), each followed by its neighbour's flag
@@ -3796,6 +3806,7 @@ int pft_slab_set_boundary_stream(pft_slab* s, int on)
   s->bnd_mode = on && eb && atoi(eb) == 1 ? 1 : 0;
   s->ce_streams = es ? atoi(es) : 2;
   if (s->ce_streams == 2 && !s->ev_copy) HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
+  if (!s->ev_side) HIPCHK(hipEventCreateWithFlags(&s->ev_side, hipEventDisableTiming));
   s->bnd_pending = 0;
   return 0;
 }

@@ -209,18 +209,21 @@ def test_lost_ipc_halo_ends_in_device_error_not_a_hang(tmp_path):
 
 # ---- the exchange on the copy engines (PFT_IPC_CE=1: pft_slab_halo_put_ce) --------------------
 
-@pytest.mark.parametrize("nranks,pair,staged,ce_ranks", [(2, 2, 0, (0, 1)), (3, 2, 0, (0, 1, 2)), (3, 2, 1, (0, 1, 2)),
-                                                          (2, 0, 0, (0, 1)), (3, 0, 1, (0, 1, 2)),
-                                                          (3, 2, 0, (1,))])
-def test_g20_processes_copy_engine_equal_reference(tmp_path, nranks, pair, staged, ce_ranks):
+@pytest.mark.parametrize("nranks,pair,staged,ce_ranks,seqtab", [(2, 2, 0, (0, 1), 0), (3, 2, 0, (0, 1, 2), 0),
+                                                                  (3, 2, 1, (0, 1, 2), 0), (2, 0, 0, (0, 1), 0),
+                                                                  (3, 0, 1, (0, 1, 2), 0), (3, 2, 0, (1,), 0),
+                                                                  (3, 2, 1, (0, 1, 2), 5)])
+def test_g20_processes_copy_engine_equal_reference(tmp_path, nranks, pair, staged, ce_ranks, seqtab):
     """the boundary planes first, their exchange as SDMA copies and 8-byte flag copies on the comm
     stream beside the interior launch, the receiver's flag wait before the next launch: golden g20
     bit for bit with the pair kernels (two-plane halo) and one launch per stage, direct and staged.
     ce_ranks (1,): only the middle rank puts on the copy engines, its neighbours with the put
-    kernel -- the receiving side is the same for both"""
+    kernel -- the receiving side is the same for both.  seqtab 5 (PFT_CE_SEQTAB): the flags' table
+    of sequence numbers refilled every 5 exchanges, hundreds of times over the run"""
     meta, A = O.load_case("g20")
     times = meta["traj_times"][:2]
-    env = {r: dict({"PFT_IPC_CE": "1"} if r in ce_ranks else {}, **({"PFT_IPC_STAGED": "1"} if staged else {}))
+    env = {r: dict({"PFT_IPC_CE": "1"} if r in ce_ranks else {}, **({"PFT_IPC_STAGED": "1"} if staged else {}),
+                   **({"PFT_CE_SEQTAB": str(seqtab)} if seqtab else {}))
            for r in range(nranks)}
     res = _run_ranks(tmp_path, nranks, rank_env=env, case="g20", times=times, tile=2, pair=pair)
     for r in res:
