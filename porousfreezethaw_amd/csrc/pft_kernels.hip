@@ -3890,6 +3890,12 @@ int pft_slab_halo_wait(pft_slab* s, unsigned long long seq)
     w.recv = 1;
     const long n = 4L * r.nf * s->plane;
     blocks = (int)std::min<long>(1024, std::max<long>(1, (n + 255) / 256));
+    // every block spins until the flags arrive: with a staged neighbour on this same GPU (the test
+    // hook PFT_IPC_STAGED between processes) a thousand spinning blocks leave no CU free for a
+    // pair kernel's workgroup (the whole register file) of the neighbour whose boundary raises the
+    // flag -- it would wait out PFT_IPC_TIMEOUT.  A few blocks then, which copy more each.
+    for (int side = 0; side < 2; ++side)
+      if (((sides >> side) & 1) && !s->peer[side].remote) blocks = std::min(blocks, 32);
   }
   if (s->wait_streamops) {
     // A/B (PFT_WAIT_STREAMOPS=1): the runtime's stream waits, then a separate receive launch
