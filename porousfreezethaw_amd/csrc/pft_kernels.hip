@@ -3822,13 +3822,16 @@ int pft_slab_set_boundary_stream(pft_slab* s, int on)
     HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
   }
   if (on && !s->ev_copy) HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
-  // env overrides for A/B: PFT_CE_BND=1 runs the boundary launch on its own stream beside the
-  // interior one (measured slower: its workgroups are dispatched interleaved with the interior's
-  // and it ends late, profiles/r05_ce_trace_*.txt); PFT_CE_STREAMS=1 puts every copy on the comm
-  // stream
+  // bnd_mode 2 (default): the pair kernels' boundary launch on its own stream beside their interior
+  // launch, which leaves CUs free (one workgroup per tile column); a stage launch's boundary runs
+  // before its interior.  Env overrides for A/B (profiles/r05_ce_ab.txt): PFT_CE_BND=0 every
+  // boundary before its interior, 1 every one beside (slower: a stage launch's interior fills the
+  // chip, the two launches' workgroups are dealt interleaved and the boundary ends late,
+  // profiles/r05_ce_trace_bnd.txt); PFT_CE_STREAMS=1 puts every copy on the comm stream, 4 on four
+  // streams (both slower)
   const char* eb = getenv("PFT_CE_BND");
   const char* es = getenv("PFT_CE_STREAMS");
-  s->bnd_mode = on && eb && (atoi(eb) == 1 || atoi(eb) == 2) ? atoi(eb) : 0;
+  s->bnd_mode = !on ? 0 : eb && atoi(eb) >= 0 && atoi(eb) <= 2 ? atoi(eb) : 2;
   s->ce_streams = es && (atoi(es) == 1 || atoi(es) == 4) ? atoi(es) : 2;
   if (s->ce_streams == 4)
     for (int i = 0; i < 2; ++i) {

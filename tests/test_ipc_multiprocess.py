@@ -209,27 +209,29 @@ def test_lost_ipc_halo_ends_in_device_error_not_a_hang(tmp_path):
 
 # ---- the exchange on the copy engines (PFT_IPC_CE=1: pft_slab_halo_put_ce) --------------------
 
-# copy-engine options (pft_slab_set_boundary_stream): boundary launches beside the interior ones
-# (PFT_CE_BND 2: the pair kernels', 1: every one) and four copy streams instead of two
-_BESIDE = {"PFT_CE_BND": "2", "PFT_CE_STREAMS": "4"}
-_BESIDE_ALL = {"PFT_CE_BND": "1", "PFT_CE_STREAMS": "4"}
+# copy-engine options (pft_slab_set_boundary_stream): by default the pair kernels' boundary launch
+# runs beside their interior launch (PFT_CE_BND 2); 0: every boundary launch before its interior,
+# 1: every one beside; PFT_CE_STREAMS 4: four copy streams instead of two
+_SERIAL = {"PFT_CE_BND": "0"}
+_BESIDE_ALL = {"PFT_CE_BND": "1"}
+_FOUR = {"PFT_CE_STREAMS": "4"}
 
 
 @pytest.mark.parametrize("nranks,pair,staged,ce_ranks,xenv", [(2, 2, 0, (0, 1), {}), (3, 2, 0, (0, 1, 2), {}),
                                                               (3, 2, 1, (0, 1, 2), {}), (2, 0, 0, (0, 1), {}),
                                                               (3, 0, 1, (0, 1, 2), {}), (3, 2, 0, (1,), {}),
                                                               (3, 2, 1, (0, 1, 2), {"PFT_CE_SEQTAB": "5"}),
-                                                              (2, 2, 0, (0, 1), _BESIDE), (3, 2, 1, (0, 1, 2), _BESIDE),
+                                                              (2, 2, 0, (0, 1), _SERIAL), (3, 2, 1, (0, 1, 2), _SERIAL),
                                                               (3, 0, 0, (0, 1, 2), _BESIDE_ALL),
-                                                              (3, 2, 1, (0, 2), _BESIDE_ALL)])
+                                                              (3, 2, 1, (0, 2), _BESIDE_ALL), (3, 2, 1, (0, 1, 2), _FOUR)])
 def test_g20_processes_copy_engine_equal_reference(tmp_path, nranks, pair, staged, ce_ranks, xenv):
     """the boundary planes first, their exchange as SDMA copies and 8-byte flag copies on the comm
     stream beside the interior launch, the receiver's flag wait before the next launch: golden g20
     bit for bit with the pair kernels (two-plane halo) and one launch per stage, direct and staged.
     ce_ranks (1,): only the middle rank puts on the copy engines, its neighbours with the put
     kernel -- the receiving side is the same for both.  PFT_CE_SEQTAB 5: the flags' table of
-    sequence numbers refilled every 5 exchanges, hundreds of times over the run.  _BESIDE(_ALL): the
-    boundary launch on its own stream beside the interior one, four copy streams"""
+    sequence numbers refilled every 5 exchanges, hundreds of times over the run.  _SERIAL,
+    _BESIDE_ALL, _FOUR: the boundary launches' placement and the copy streams"""
     meta, A = O.load_case("g20")
     times = meta["traj_times"][:2]
     env = {r: dict({"PFT_IPC_CE": "1"} if r in ce_ranks else {}, **({"PFT_IPC_STAGED": "1"} if staged else {}),
@@ -248,7 +250,7 @@ def test_g20_processes_copy_engine_equal_reference(tmp_path, nranks, pair, stage
         assert np.array_equal(full, A[f"traj_m0_state{i}"])
 
 
-@pytest.mark.parametrize("staged,xenv", [(0, {}), (1, {}), (0, _BESIDE), (1, _BESIDE)])
+@pytest.mark.parametrize("staged,xenv", [(0, {}), (1, {}), (0, _SERIAL), (1, _SERIAL)])
 def test_400_processes_copy_engine_equal_one_slab(tmp_path, staged, xenv):
     """400^3 over 2 processes with the pair kernels, the exchange on the copy engines"""
     steps = 10
@@ -268,7 +270,7 @@ def test_400_processes_copy_engine_equal_one_slab(tmp_path, staged, xenv):
     assert np.array_equal(np.concatenate([r["states"][0] for r in res], axis=1), x)
 
 
-@pytest.mark.parametrize("xenv", [{}, _BESIDE, _BESIDE_ALL])
+@pytest.mark.parametrize("xenv", [{}, _SERIAL, _BESIDE_ALL])
 @pytest.mark.parametrize("staged", [0, 1])
 @pytest.mark.parametrize("pair", [2, 0])
 def test_ipc_copy_engine_self_exchange_equals_reference(pair, staged, xenv, monkeypatch):
