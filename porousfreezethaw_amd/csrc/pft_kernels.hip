@@ -2035,6 +2035,7 @@ struct pft_slab {
   long part_cap;                     // ... their capacity in workgroups
   int defer_n;                       // workgroups of the armed error-norm launch awaiting reduction
   int defer_slot;                    // ... and its host slot
+  int split_pub;                     // a split stage 4+5's boundary launch armed it; the interior follows
   // host-side memos (a small slab is host-bound: ~5 launches of a few us per attempted step)
   int fgeo_valid, fgeo_wx, fgeo_ty;  // fused_geometry(n1, n2) of this slab
   double fgeo_eff;
@@ -2645,13 +2646,13 @@ int pft_slab_stage_fields(const pft_slab* s, int stage)
 
 // arm the deferred publication of an error-norm launch of nwg workgroups into host slot j: its
 // workgroups store partials (eps_store_part), the next stage-1 launch reduces and publishes them
-static int defer_arm(pft_slab* s, long nwg, int j, unsigned long long** part)
+static int defer_arm(pft_slab* s, long nwg, int j, unsigned long long** part, long cap_nwg = 0)
 {
-  if (nwg > s->part_cap) {
+  if (std::max(nwg, cap_nwg) > s->part_cap) {
     if (s->part) HIPCHK(hipFree(s->part));
     s->part = nullptr;
     s->part_cap = 0;
-    const long cap = std::max(nwg, 4096L);
+    const long cap = std::max(std::max(nwg, cap_nwg), 4096L);
     HIPCHK(hipMalloc((void**)&s->part, 16 * (size_t)cap));
     s->part_cap = cap;
   }
@@ -3046,12 +3047,19 @@ int pft_slab_set_inkernel_publish(pft_slab* s, int on)
 {
   s->inkernel_pub = on ? 1 : 0;
   s->pub_armed = 0;
+  s->split_pub = 0;
   s->defer_n = 0;
   return 0;
 }
 
 int pft_slab_eps_mark_on(pft_slab* s, void* stream)
 {
+  if (s->split_pub) {
+    // a split stage 4+5 whose interior launch had no planes: the boundary's partials are all
+    s->split_pub = 0;
+    s->pub_armed = 1;
+    s->pub_slot = s->defer_slot;
+  }
   if (s->pub_armed && stream == (void*)s->stream) {
     // the stage-5 launch just enqueued publishes the error norm itself
     s->pub_armed = 0;
@@ -3451,6 +3459,8 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
                    (s->gl_keep && std::isfinite(a.cinA) && std::isfinite(a.cinB) && std::isfinite(coef));
   a.gl_keep = glx ? 1 : 0;
   s->pub_armed = 0;
+  const int split_pub = s->split_pub;
+  s->split_pub = 0;
   if (first == 4 && s->inkernel_pub && !bnd && k_begin == 0 && k_end == s->d.n3) {
     const int j = (int)(s->pub_next % PFT_PUB_SLOTS);
     __atomic_store_n(&s->pub_ring[2 * j], PFT_PUB_SENTINEL, __ATOMIC_RELEASE);
@@ -3459,6 +3469,22 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
     if (rc) return rc;
     s->pub_armed = 1;
     s->pub_slot = j;
+  } else if (first == 4 && s->inkernel_pub && bnd) {
+    // split stage 4+5 (boundary, then interior: rk_solver do_pair): the boundary launch's partials
+    // first, the interior's after them (the capacity for both now: no reallocation between the two
+    // launches), reduced and published by the next stage-1 launch as for one launch
+    const int j = (int)(s->pub_next % PFT_PUB_SLOTS);
+    __atomic_store_n(&s->pub_ring[2 * j], PFT_PUB_SENTINEL, __ATOMIC_RELEASE);
+    __atomic_store_n(&s->pub_ring[2 * j + 1], PFT_PUB_SENTINEL, __ATOMIC_RELEASE);
+    const int rc = defer_arm(s, (long)a.ntile * a.nchunk, j, &a.part, (long)a.ntile * (a.nchunk + s->d.n3));
+    if (rc) return rc;
+    s->split_pub = 1;
+  } else if (first == 4 && split_pub && !bnd && s->defer_n > 0 &&
+             s->defer_n + (long)a.ntile * a.nchunk <= s->part_cap) {
+    a.part = s->part + 2 * (long)s->defer_n;
+    s->defer_n += a.ntile * a.nchunk;
+    s->pub_armed = 1;
+    s->pub_slot = s->defer_slot;
   }
   const dim3 g((unsigned)(a.ntile * a.nchunk));
   hipStream_t st = s->stream;
