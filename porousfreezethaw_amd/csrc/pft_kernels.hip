@@ -1995,7 +1995,7 @@ struct pft_slab {
   // a launch of the boundary planes (PFT_K_BOUNDARY/2) runs on `bnd` beside the interior launch on
   // the compute stream instead of before it; the exchange waits for ev_bnd, and so does the compute
   // stream before the next launch (pft_slab_halo_wait).  bnd_mode 1: every boundary launch, 2: the
-  // pair kernels' only (their interior launch leaves CUs free, run_pair)
+  // pair kernels' where their interior launch leaves CUs free, 3: every pair kernel's (run_pair)
   int bnd_mode, bnd_pending, ce_streams;
   hipStream_t ce_x[2];   // ce_streams 4: the second copy stream of each side (below, above)
   hipEvent_t ev_x[2];
@@ -3488,10 +3488,20 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
   }
   const dim3 g((unsigned)(a.ntile * a.nchunk));
   hipStream_t st = s->stream;
-  // bnd_mode 1 or 2: the boundary launch beside the interior one, which holds a workgroup per tile
-  // column (ntile workgroups, one per CU: on a 400 x 400 plane 220 of 256 CUs); the boundary's
-  // workgroups take the CUs it leaves, and the copies start while the interior still runs
-  if (bnd && s->bnd_mode) {
+  // bnd_mode 1-3: the boundary launch beside the interior one where that leaves CUs free -- on a
+  // 400 x 400 plane one workgroup per tile column, 220 of 256 CUs: the boundary's workgroups take
+  // the CUs it leaves, and the copies start while the interior still runs.  An interior launch of
+  // more workgroups than CUs (several rounds) leaves none until its last round: in bnd_mode 2 its
+  // boundary then runs before it (profiles/r05_ce_shapes.txt)
+  bool beside = bnd && s->bnd_mode != 0;
+  if (beside && s->bnd_mode == 2) {
+    const int ni = s->d.n3 - 4;
+    const int occ = first == 2 ? pair_occupancy_mode<2, false>(mode) : pair_occupancy_mode<4, false>(mode);
+    const int kzi = s->kz > 0 ? s->kz : chunk_kz(s, 12 + (first == 4 ? 1 : 0), occ, a.ntile, ni);
+    const long nbi = (long)a.ntile * ((ni + kzi - 1) / kzi);
+    beside = nbi + 16 <= (long)s->n_cu * occ;
+  }
+  if (beside) {
     HIPCHK(hipEventRecord(s->ev_pre, s->stream));
     HIPCHK(hipStreamWaitEvent(s->bnd, s->ev_pre, 0));
     st = s->bnd;
@@ -3505,7 +3515,7 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
     else launch_pair_mode<4, false>(mode, lwp, g, st, a, s->c);
   }
   HIPCHK(hipGetLastError());
-  if (bnd && s->bnd_mode) {
+  if (beside) {
     HIPCHK(hipEventRecord(s->ev_bnd, s->bnd));
     s->bnd_pending = 1;
   }
@@ -3849,15 +3859,15 @@ int pft_slab_set_boundary_stream(pft_slab* s, int on)
   }
   if (on && !s->ev_copy) HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
   // bnd_mode 2 (default): the pair kernels' boundary launch on its own stream beside their interior
-  // launch, which leaves CUs free (one workgroup per tile column); a stage launch's boundary runs
-  // before its interior.  Env overrides for A/B (profiles/r05_ce_ab.txt): PFT_CE_BND=0 every
+  // launch where that leaves CUs free (one workgroup per tile column, run_pair); 3: beside every
+  // pair interior; a stage launch's boundary runs before its interior.  Env overrides for A/B (profiles/r05_ce_ab.txt): PFT_CE_BND=0 every
   // boundary before its interior, 1 every one beside (slower: a stage launch's interior fills the
   // chip, the two launches' workgroups are dealt interleaved and the boundary ends late,
   // profiles/r05_ce_trace_bnd.txt); PFT_CE_STREAMS=1 puts every copy on the comm stream, 4 on four
   // streams (both slower)
   const char* eb = getenv("PFT_CE_BND");
   const char* es = getenv("PFT_CE_STREAMS");
-  s->bnd_mode = !on ? 0 : eb && atoi(eb) >= 0 && atoi(eb) <= 2 ? atoi(eb) : 2;
+  s->bnd_mode = !on ? 0 : eb && atoi(eb) >= 0 && atoi(eb) <= 3 ? atoi(eb) : 2;
   s->ce_streams = es && (atoi(es) == 1 || atoi(es) == 4) ? atoi(es) : 2;
   if (s->ce_streams == 4)
     for (int i = 0; i < 2; ++i) {
