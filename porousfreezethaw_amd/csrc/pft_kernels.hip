@@ -1997,8 +1997,6 @@ struct pft_slab {
   // stream before the next launch (pft_slab_halo_wait).  bnd_mode 1: every boundary launch, 2: the
   // pair kernels' where their interior launch leaves CUs free, 3: every pair kernel's (run_pair)
   int bnd_mode, bnd_pending, ce_streams;
-  hipStream_t ce_x[2];   // ce_streams 4: the second copy stream of each side (below, above)
-  hipEvent_t ev_x[2];
   int ce_marked;         // pft_slab_halo_mark recorded ev_order[0] after the launch the next put_ce sends
   int wait_streamops;    // A/B: halo waits as hipStreamWaitValue64 (env PFT_WAIT_STREAMOPS=1)
   hipStream_t bnd;
@@ -2345,10 +2343,7 @@ int pft_slab_destroy(pft_slab* s)
   if (s->ev_pre) (void)hipEventDestroy(s->ev_pre);
   if (s->ev_copy) (void)hipEventDestroy(s->ev_copy);
   if (s->ev_side) (void)hipEventDestroy(s->ev_side);
-  for (int i = 0; i < 2; ++i) {
-    if (s->ce_x[i]) (void)hipStreamDestroy(s->ce_x[i]);
-    if (s->ev_x[i]) (void)hipEventDestroy(s->ev_x[i]);
-  }
+
   if (s->ev_eps) (void)hipEventDestroy(s->ev_eps);
   for (int i = 0; i < 3; ++i)
     if (s->ev_order[i]) (void)hipEventDestroy(s->ev_order[i]);
@@ -3664,8 +3659,7 @@ int pft_slab_ipc_close(pft_slab* s)
     (void)hipStreamSynchronize(s->stream);
     (void)hipStreamSynchronize(s->side);
     if (s->bnd) (void)hipStreamSynchronize(s->bnd);
-    for (int i = 0; i < 2; ++i)
-      if (s->ce_x[i]) (void)hipStreamSynchronize(s->ce_x[i]);
+
     (void)hipStreamSynchronize(s->comm);
     HIPCHK(hipMemset(s->sig, 0, 2 * sizeof(unsigned long long)));
     HIPCHK(hipDeviceSynchronize());
@@ -3785,17 +3779,14 @@ int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsign
     HIPCHK(hipMemcpyAsync(s->seqtab, h, sizeof(unsigned long long) * NSEQ, hipMemcpyHostToDevice, s->comm));
   }
   // the planes to the neighbour below go on the comm stream, to the one above on the side stream
-  // (two copy engines; ce_streams = 1: all on the comm stream), each followed by its neighbour's flag;
-  // ce_streams = 4: every other copy of a side on that side's second stream (ce_x), which the flag
-  // copy then waits for
+  // (two copy engines; ce_streams = 1: all on the comm stream), each followed by its neighbour's
+  // flag.  (Four streams, a side's copies alternating between two, measured slower: 11 300-12 600
+  // against 16 000 Mcells*steps/s on the 800^3 rank slab, profiles/r05_ce_ab.txt; removed.)
   hipStream_t cs[2] = {s->comm, s->ce_streams == 1 ? s->comm : s->side};
-  hipStream_t cx[2] = {s->ce_streams == 4 ? s->ce_x[0] : cs[0], s->ce_streams == 4 ? s->ce_x[1] : cs[1]};
   hipEvent_t ready = s->bnd_pending ? s->ev_bnd : s->ev_order[0];
   if (!s->bnd_pending && !marked) HIPCHK(hipEventRecord(s->ev_order[0], s->stream));
   HIPCHK(hipStreamWaitEvent(cs[0], ready, 0));
   if (cs[1] != cs[0]) HIPCHK(hipStreamWaitEvent(cs[1], ready, 0));
-  for (int side = 0; side < 2; ++side)
-    if (cx[side] != cs[side] && s->peer[side].on) HIPCHK(hipStreamWaitEvent(cx[side], ready, 0));
   const int ph = s->phys[role];
   const long P = s->plane, n3 = s->d.n3;
   const long slot = (long)(seq & 1) * 12 * P;
@@ -3803,7 +3794,6 @@ int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsign
   for (int side = 0; side < 2; ++side) {
     const SlabPeer& p = s->peer[side];
     if (!p.on) continue;
-    int nc = 0;   // copies of this side so far: odd ones on cx[side]
     for (int q = f0; q < f1; ++q) {
       const double* src = s->buf[role] + q * s->fs;
       if (!p.staged) {
@@ -3811,21 +3801,16 @@ int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsign
         // into its (far -1,) ghost 0 -- contiguous on both ends
         double* dst = side == 0 ? p.base[ph] + q * p.fs + (p.n3 + 1) * P : p.base[ph] + q * p.fs - (deep ? P : 0);
         const double* sp = side == 0 ? src + P : src + (deep ? n3 - 1 : n3) * P;
-        HIPCHK(hipMemcpyAsync(dst, sp, (deep ? 2 : 1) * pb, hipMemcpyDeviceToDeviceNoCU, (nc++ & 1) ? cx[side] : cs[side]));
+        HIPCHK(hipMemcpyAsync(dst, sp, (deep ? 2 : 1) * pb, hipMemcpyDeviceToDeviceNoCU, cs[side]));
       } else {
         // its receive buffer [slot][side][depth][field][plane]: the neighbour below receives our
         // planes as "from above" (side 1), the one above as "from below" (side 0)
         for (int d = 0; d < (deep ? 2 : 1); ++d) {
           double* dst = p.rbuf + slot + ((long)((side == 0 ? 1 : 0) * 2 + d) * 3 + q) * P;
           const double* sp = side == 0 ? src + (1 + d) * P : src + (n3 - d) * P;
-          HIPCHK(hipMemcpyAsync(dst, sp, pb, hipMemcpyDeviceToDeviceNoCU, (nc++ & 1) ? cx[side] : cs[side]));
+          HIPCHK(hipMemcpyAsync(dst, sp, pb, hipMemcpyDeviceToDeviceNoCU, cs[side]));
         }
       }
-    }
-    if (cx[side] != cs[side] && nc > 1) {
-      // the flag follows both streams' copies
-      HIPCHK(hipEventRecord(s->ev_x[side], cx[side]));
-      HIPCHK(hipStreamWaitEvent(cs[side], s->ev_x[side], 0));
     }
   }
   const unsigned long long* sv = s->seqtab + (seq - 1 - s->seq_base);
@@ -3863,17 +3848,11 @@ int pft_slab_set_boundary_stream(pft_slab* s, int on)
   // pair interior; a stage launch's boundary runs before its interior.  Env overrides for A/B (profiles/r05_ce_ab.txt): PFT_CE_BND=0 every
   // boundary before its interior, 1 every one beside (slower: a stage launch's interior fills the
   // chip, the two launches' workgroups are dealt interleaved and the boundary ends late,
-  // profiles/r05_ce_trace_bnd.txt); PFT_CE_STREAMS=1 puts every copy on the comm stream, 4 on four
-  // streams (both slower)
+  // profiles/r05_ce_trace_bnd.txt); PFT_CE_STREAMS=1 puts every copy on the comm stream (slower)
   const char* eb = getenv("PFT_CE_BND");
   const char* es = getenv("PFT_CE_STREAMS");
   s->bnd_mode = !on ? 0 : eb && atoi(eb) >= 0 && atoi(eb) <= 3 ? atoi(eb) : 2;
-  s->ce_streams = es && (atoi(es) == 1 || atoi(es) == 4) ? atoi(es) : 2;
-  if (s->ce_streams == 4)
-    for (int i = 0; i < 2; ++i) {
-      if (!s->ce_x[i]) HIPCHK(hipStreamCreateWithFlags(&s->ce_x[i], hipStreamNonBlocking));
-      if (!s->ev_x[i]) HIPCHK(hipEventCreateWithFlags(&s->ev_x[i], hipEventDisableTiming));
-    }
+  s->ce_streams = es && atoi(es) == 1 ? 1 : 2;
   if (s->ce_streams == 2 && !s->ev_copy) HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
   if (!s->ev_side) HIPCHK(hipEventCreateWithFlags(&s->ev_side, hipEventDisableTiming));
   s->bnd_pending = 0;

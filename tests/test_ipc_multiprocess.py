@@ -211,12 +211,10 @@ def test_lost_ipc_halo_ends_in_device_error_not_a_hang(tmp_path):
 
 # copy-engine options (pft_slab_set_boundary_stream): by default the pair kernels' boundary launch
 # runs beside their interior launch where that leaves CUs free (PFT_CE_BND 2); 0: every boundary
-# launch before its interior, 1: every one beside, 3: every pair kernel's beside; PFT_CE_STREAMS 4:
-# four copy streams instead of two
+# launch before its interior, 1: every one beside, 3: every pair kernel's beside
 _SERIAL = {"PFT_CE_BND": "0"}
 _BESIDE_PAIRS = {"PFT_CE_BND": "3"}
 _BESIDE_ALL = {"PFT_CE_BND": "1"}
-_FOUR = {"PFT_CE_STREAMS": "4"}
 
 
 @pytest.mark.parametrize("nranks,pair,staged,ce_ranks,xenv", [(2, 2, 0, (0, 1), {}), (3, 2, 0, (0, 1, 2), {}),
@@ -225,7 +223,7 @@ _FOUR = {"PFT_CE_STREAMS": "4"}
                                                               (3, 2, 1, (0, 1, 2), {"PFT_CE_SEQTAB": "5"}),
                                                               (2, 2, 0, (0, 1), _SERIAL), (3, 2, 1, (0, 1, 2), _SERIAL),
                                                               (3, 0, 0, (0, 1, 2), _BESIDE_ALL),
-                                                              (3, 2, 1, (0, 2), _BESIDE_ALL), (3, 2, 1, (0, 1, 2), _FOUR)])
+                                                              (3, 2, 1, (0, 2), _BESIDE_ALL)])
 def test_g20_processes_copy_engine_equal_reference(tmp_path, nranks, pair, staged, ce_ranks, xenv):
     """the boundary planes first, their exchange as SDMA copies and 8-byte flag copies on the comm
     stream beside the interior launch, the receiver's flag wait before the next launch: golden g20
@@ -233,7 +231,7 @@ def test_g20_processes_copy_engine_equal_reference(tmp_path, nranks, pair, stage
     ce_ranks (1,): only the middle rank puts on the copy engines, its neighbours with the put
     kernel -- the receiving side is the same for both.  PFT_CE_SEQTAB 5: the flags' table of
     sequence numbers refilled every 5 exchanges, hundreds of times over the run.  _SERIAL,
-    _BESIDE_ALL, _FOUR: the boundary launches' placement and the copy streams"""
+    _BESIDE_ALL: the boundary launches' placement"""
     meta, A = O.load_case("g20")
     times = meta["traj_times"][:2]
     env = {r: dict({"PFT_IPC_CE": "1"} if r in ce_ranks else {}, **({"PFT_IPC_STAGED": "1"} if staged else {}),
