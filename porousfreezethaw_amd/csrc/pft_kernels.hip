@@ -1995,7 +1995,7 @@ struct pft_slab {
   // a launch of the boundary planes (PFT_K_BOUNDARY/2) runs on `bnd` beside the interior launch on
   // the compute stream instead of before it; the exchange waits for ev_bnd, and so does the compute
   // stream before the next launch (pft_slab_halo_wait).  bnd_mode 1: every boundary launch, 2: the
-  // pair kernels' where their interior launch leaves CUs free, 3: every pair kernel's (run_pair)
+  // pair kernels' (run_pair)
   int bnd_mode, bnd_pending, ce_streams;
   int ce_marked;         // pft_slab_halo_mark recorded ev_order[0] after the launch the next put_ce sends
   int wait_streamops;    // A/B: halo waits as hipStreamWaitValue64 (env PFT_WAIT_STREAMOPS=1)
@@ -3483,19 +3483,12 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
   }
   const dim3 g((unsigned)(a.ntile * a.nchunk));
   hipStream_t st = s->stream;
-  // bnd_mode 1-3: the boundary launch beside the interior one where that leaves CUs free -- on a
-  // 400 x 400 plane one workgroup per tile column, 220 of 256 CUs: the boundary's workgroups take
-  // the CUs it leaves, and the copies start while the interior still runs.  An interior launch of
-  // more workgroups than CUs (several rounds) leaves none until its last round: in bnd_mode 2 its
-  // boundary then runs before it (profiles/r05_ce_shapes.txt)
-  bool beside = bnd && s->bnd_mode != 0;
-  if (beside && s->bnd_mode == 2) {
-    const int ni = s->d.n3 - 4;
-    const int occ = first == 2 ? pair_occupancy_mode<2, false>(mode) : pair_occupancy_mode<4, false>(mode);
-    const int kzi = s->kz > 0 ? s->kz : chunk_kz(s, 12 + (first == 4 ? 1 : 0), occ, a.ntile, ni);
-    const long nbi = (long)a.ntile * ((ni + kzi - 1) / kzi);
-    beside = nbi + 16 <= (long)s->n_cu * occ;
-  }
+  // bnd_mode 1, 2: the boundary launch beside the interior one.  On a 400 x 400 plane the interior
+  // holds one workgroup per tile column, 220 of 256 CUs: the boundary's workgroups take the CUs it
+  // leaves and the copies start while the interior still runs.  An interior launch of more
+  // workgroups than CUs (several rounds, the 318^2 and 252^2 planes) leaves CUs only in its last
+  // round, and beside is still no slower there than before (profiles/r05_ce_shapes.txt)
+  const bool beside = bnd && s->bnd_mode != 0;
   if (beside) {
     HIPCHK(hipEventRecord(s->ev_pre, s->stream));
     HIPCHK(hipStreamWaitEvent(s->bnd, s->ev_pre, 0));
@@ -3844,14 +3837,13 @@ int pft_slab_set_boundary_stream(pft_slab* s, int on)
   }
   if (on && !s->ev_copy) HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
   // bnd_mode 2 (default): the pair kernels' boundary launch on its own stream beside their interior
-  // launch where that leaves CUs free (one workgroup per tile column, run_pair); 3: beside every
-  // pair interior; a stage launch's boundary runs before its interior.  Env overrides for A/B (profiles/r05_ce_ab.txt): PFT_CE_BND=0 every
+  // launch (run_pair); a stage launch's boundary runs before its interior.  Env overrides for A/B (profiles/r05_ce_ab.txt): PFT_CE_BND=0 every
   // boundary before its interior, 1 every one beside (slower: a stage launch's interior fills the
   // chip, the two launches' workgroups are dealt interleaved and the boundary ends late,
   // profiles/r05_ce_trace_bnd.txt); PFT_CE_STREAMS=1 puts every copy on the comm stream (slower)
   const char* eb = getenv("PFT_CE_BND");
   const char* es = getenv("PFT_CE_STREAMS");
-  s->bnd_mode = !on ? 0 : eb && atoi(eb) >= 0 && atoi(eb) <= 3 ? atoi(eb) : 2;
+  s->bnd_mode = !on ? 0 : eb && atoi(eb) >= 0 && atoi(eb) <= 2 ? atoi(eb) : 2;
   s->ce_streams = es && atoi(es) == 1 ? 1 : 2;
   if (s->ce_streams == 2 && !s->ev_copy) HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
   if (!s->ev_side) HIPCHK(hipEventCreateWithFlags(&s->ev_side, hipEventDisableTiming));

@@ -210,10 +210,9 @@ def test_lost_ipc_halo_ends_in_device_error_not_a_hang(tmp_path):
 # ---- the exchange on the copy engines (PFT_IPC_CE=1: pft_slab_halo_put_ce) --------------------
 
 # copy-engine options (pft_slab_set_boundary_stream): by default the pair kernels' boundary launch
-# runs beside their interior launch where that leaves CUs free (PFT_CE_BND 2); 0: every boundary
-# launch before its interior, 1: every one beside, 3: every pair kernel's beside
+# runs beside their interior launch (PFT_CE_BND 2); 0: every boundary launch before its interior,
+# 1: every one beside
 _SERIAL = {"PFT_CE_BND": "0"}
-_BESIDE_PAIRS = {"PFT_CE_BND": "3"}
 _BESIDE_ALL = {"PFT_CE_BND": "1"}
 
 
@@ -250,8 +249,7 @@ def test_g20_processes_copy_engine_equal_reference(tmp_path, nranks, pair, stage
         assert np.array_equal(full, A[f"traj_m0_state{i}"])
 
 
-@pytest.mark.parametrize("staged,xenv", [(0, {}), (1, {}), (0, _SERIAL), (1, _SERIAL), (0, _BESIDE_PAIRS),
-                                         (1, _BESIDE_PAIRS)])
+@pytest.mark.parametrize("staged,xenv", [(0, {}), (1, {}), (0, _SERIAL), (1, _SERIAL)])
 def test_400_processes_copy_engine_equal_one_slab(tmp_path, staged, xenv):
     """400^3 over 2 processes with the pair kernels, the exchange on the copy engines"""
     steps = 10
@@ -271,7 +269,7 @@ def test_400_processes_copy_engine_equal_one_slab(tmp_path, staged, xenv):
     assert np.array_equal(np.concatenate([r["states"][0] for r in res], axis=1), x)
 
 
-@pytest.mark.parametrize("xenv", [{}, _SERIAL, _BESIDE_ALL, _BESIDE_PAIRS])
+@pytest.mark.parametrize("xenv", [{}, _SERIAL, _BESIDE_ALL])
 @pytest.mark.parametrize("staged", [0, 1])
 @pytest.mark.parametrize("pair", [2, 0])
 def test_ipc_copy_engine_self_exchange_equals_reference(pair, staged, xenv, monkeypatch):
