@@ -57,6 +57,9 @@ typedef struct {
 int pft_hip_device_count(int * n);
 int pft_hip_set_device(int dev);
 int pft_hip_get_device(int * dev);
+/* the GPU's PCI location (domain, bus, device) as one integer: equal across processes exactly when
+   they use the same physical GPU (the ipc transport's staged-or-direct decision) */
+int pft_hip_device_phys_id(int dev, int * id);
 int pft_hip_device_sync(void);
 const char * pft_hip_last_error(void);
 

@@ -472,7 +472,9 @@ static int ipc_attach(pft_comm* c, pft_slab* s)
   IpcSlot* me = &c->shm->slot[c->rank];
   int lrc = pft_slab_ipc_export(s, me->handles);
   me->n3 = pft_slab_nz(s);
-  me->device = c->device;
+  // the GPU's physical id, not the index: ranks whose device numbering differs (HIP_VISIBLE_DEVICES
+  // per rank) still see whether a neighbour shares their GPU (pft_slab_ipc_set_peer: staged or not)
+  if (!lrc) lrc = pft_hip_device_phys_id(c->device, &me->device);
   me->fs = (long)pft_slab_field_stride(s);
   me->staged = pft_ipc_staged_env();
   if ((rc = ipc_round(c, nullptr, lrc ? 1 : 0, nullptr, 0, &recs))) return rc;   // every slot is published

@@ -2212,6 +2212,18 @@ int pft_hip_get_device(int* dev)
   HIPCHK(hipGetDevice(dev));
   return 0;
 }
+
+int pft_hip_device_phys_id(int dev, int* id)
+{
+  // the GPU's PCI location (domain, bus, device): the same physical GPU has the same id in every
+  // process, whatever each process's device numbering (HIP_VISIBLE_DEVICES)
+  int dom = 0, bus = 0, pdev = 0;
+  HIPCHK(hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainId, dev));
+  HIPCHK(hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, dev));
+  HIPCHK(hipDeviceGetAttribute(&pdev, hipDeviceAttributePciDeviceId, dev));
+  *id = ((dom & 0xffff) << 13) | ((bus & 0xff) << 5) | (pdev & 0x1f);
+  return 0;
+}
 int pft_hip_device_sync(void)
 {
   HIPCHK(hipDeviceSynchronize());
@@ -3614,8 +3626,10 @@ int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, lo
     p.on = 1;
     return 0;
   }
-  int mine = 0;
-  HIPCHK(hipGetDevice(&mine));
+  // `device`: the peer GPU's pft_hip_device_phys_id, compared with ours
+  int mine = 0, dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  if (pft_hip_device_phys_id(dev, &mine)) return -1;
   const hipIpcMemHandle_t* h = (const hipIpcMemHandle_t*)handles;
   for (int b = 0; b <= PFT_BUF_COUNT + 1; ++b) {
     void* ptr = nullptr;

@@ -342,3 +342,19 @@ def test_failed_attach_fails_every_rank_at_once(tmp_path):
     for r, p in enumerate(procs):
         assert p.returncode != 0 and "RK_MPI_SA_init failed" in outs[r], outs[r][-2000:]
     assert el < 90, el          # the import of torch-free workers plus the failed attach, not the 120 s bound
+
+
+@pytest.mark.gpu
+def test_device_phys_id_names_the_gpu():
+    """pft_hip_device_phys_id: the PCI location, stable, distinct per visible GPU -- the ipc
+    transport compares it (not the device index) to decide whether a neighbour shares the GPU"""
+    import ctypes as C
+    import torch
+    L = P.lib()
+    ids = []
+    for d in range(torch.cuda.device_count()):
+        a, b = C.c_int(-1), C.c_int(-2)
+        assert L.pft_hip_device_phys_id(d, C.byref(a)) == 0 and L.pft_hip_device_phys_id(d, C.byref(b)) == 0
+        assert a.value == b.value and a.value >= 0
+        ids.append(a.value)
+    assert len(set(ids)) == len(ids)
