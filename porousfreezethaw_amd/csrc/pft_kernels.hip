@@ -1995,12 +1995,12 @@ struct pft_slab {
   // a launch of the boundary planes (PFT_K_BOUNDARY/2) runs on `bnd` beside the interior launch on
   // the compute stream instead of before it; the exchange waits for ev_bnd, and so does the compute
   // stream before the next launch (pft_slab_halo_wait).  bnd_mode 1: every boundary launch, 2: the
-  // pair kernels' (run_pair)
+  // pair kernels' (run_pair), 3: every one, with the halo waits on `bnd` (the boundary pipeline)
   int bnd_mode, bnd_pending, ce_streams;
   int ce_marked;         // pft_slab_halo_mark recorded ev_order[0] after the launch the next put_ce sends
   int wait_streamops;    // A/B: halo waits as hipStreamWaitValue64 (env PFT_WAIT_STREAMOPS=1)
   hipStream_t bnd;
-  hipEvent_t ev_bnd, ev_pre, ev_copy, ev_side;
+  hipEvent_t ev_bnd, ev_pre, ev_copy, ev_side, ev_join;
   int put_role, put_f0, put_f1, put_deep;   // the exchange the last halo_put2 sent (its wait receives it)
   SlabPeer peer[2];              // [0] the neighbour below, [1] above
   int drop_puts;                 // fault injection: halo puts and flag raises skipped (PFT_IPC_DROP_PUTS)
@@ -2155,6 +2155,12 @@ static int slab_wait(pft_slab* s, hipEvent_t ev, const char* what)
     if (s->ipc_poisoned == 1) (void)hipStreamSynchronize(s->stream);
     (void)hipGetLastError();
     return slab_poisoned(s, what);
+  }
+  if (!ev && s->bnd_mode == 3 && s->bnd && s->ev_join) {
+    // the boundary pipeline: a wait for the compute stream includes the boundary stream (its
+    // halo waits and staged receives write ghost planes the host or the next call may read)
+    HIPCHK(hipEventRecord(s->ev_join, s->bnd));
+    HIPCHK(hipStreamWaitEvent(s->stream, s->ev_join, 0));
   }
   if (!s->peer[0].on && !s->peer[1].on && !s->watch) {
     HIPCHK(ev ? hipEventSynchronize(ev) : hipStreamSynchronize(s->stream));
@@ -2355,6 +2361,7 @@ int pft_slab_destroy(pft_slab* s)
   if (s->ev_pre) (void)hipEventDestroy(s->ev_pre);
   if (s->ev_copy) (void)hipEventDestroy(s->ev_copy);
   if (s->ev_side) (void)hipEventDestroy(s->ev_side);
+  if (s->ev_join) (void)hipEventDestroy(s->ev_join);
 
   if (s->ev_eps) (void)hipEventDestroy(s->ev_eps);
   for (int i = 0; i < 3; ++i)
@@ -2782,7 +2789,12 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   }
   dim3 g((unsigned)(a.ntile * a.nchunk));
   bool extra = false;
-  if (stage == 1 && kind == KFUSED && s->defer_n > 0) {
+  // a stage launch's interior fills the chip: its boundary runs beside it only in bnd_mode 1 and 3
+  // (3: the boundary pipeline, pft_slab_halo_wait)
+  const bool beside = bnd && (s->bnd_mode == 1 || s->bnd_mode == 3);
+  // the reduction of the previous error-norm launch's partials needs that launch complete: in the
+  // pipeline a boundary launch may run beside its end, so the interior launch takes it
+  if (stage == 1 && kind == KFUSED && s->defer_n > 0 && !(beside && s->bnd_mode == 3)) {
     // the previous error-norm launch's partials: reduced and published by one extra workgroup
     a.part = s->part;
     a.npart = s->defer_n;
@@ -2811,8 +2823,6 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   }
   if (extra) g.x += 1;
   hipStream_t st = s->stream;
-  // a stage launch's interior fills the chip: its boundary runs beside it only in bnd_mode 1
-  const bool beside = bnd && s->bnd_mode == 1;
   if (beside) {
     HIPCHK(hipEventRecord(s->ev_pre, s->stream));
     HIPCHK(hipStreamWaitEvent(s->bnd, s->ev_pre, 0));
@@ -3851,16 +3861,19 @@ int pft_slab_set_boundary_stream(pft_slab* s, int on)
   }
   if (on && !s->ev_copy) HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
   // bnd_mode 2 (default): the pair kernels' boundary launch on its own stream beside their interior
-  // launch (run_pair); a stage launch's boundary runs before its interior.  Env overrides for A/B (profiles/r05_ce_ab.txt): PFT_CE_BND=0 every
+  // launch (run_pair); a stage launch's boundary runs before its interior.  3: the boundary
+  // pipeline -- every boundary launch beside its interior, and the halo waits on the boundary
+  // stream (pft_slab_halo_wait), so that no interior launch waits for a neighbour's flag.  Env overrides for A/B (profiles/r05_ce_ab.txt): PFT_CE_BND=0 every
   // boundary before its interior, 1 every one beside (slower: a stage launch's interior fills the
   // chip, the two launches' workgroups are dealt interleaved and the boundary ends late,
   // profiles/r05_ce_trace_bnd.txt); PFT_CE_STREAMS=1 puts every copy on the comm stream (slower)
   const char* eb = getenv("PFT_CE_BND");
   const char* es = getenv("PFT_CE_STREAMS");
-  s->bnd_mode = !on ? 0 : eb && atoi(eb) >= 0 && atoi(eb) <= 2 ? atoi(eb) : 2;
+  s->bnd_mode = !on ? 0 : eb && atoi(eb) >= 0 && atoi(eb) <= 3 ? atoi(eb) : 2;
   s->ce_streams = es && atoi(es) == 1 ? 1 : 2;
   if (s->ce_streams == 2 && !s->ev_copy) HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
   if (!s->ev_side) HIPCHK(hipEventCreateWithFlags(&s->ev_side, hipEventDisableTiming));
+  if (!s->ev_join) HIPCHK(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
   s->bnd_pending = 0;
   return 0;
 }
@@ -3882,10 +3895,15 @@ int pft_slab_halo_wait(pft_slab* s, unsigned long long seq)
 {
   // flags [0] (from below) and [1] (from above): the stream goes on once both planes are in
   if (s->ipc_poisoned) return slab_poisoned(s, "pft_slab_halo_wait");
+  // the boundary pipeline (bnd_mode 3): after a boundary launch beside the interior, the flags are
+  // waited for on the boundary stream -- only the next boundary launch (after this wait on that
+  // stream) reads ghost planes; the next interior launch waits for this boundary launch alone
+  hipStream_t ws = s->stream;
   if (s->bnd_pending) {
     // the boundary launch ran beside the interior one: its planes are the next launch's input
     HIPCHK(hipStreamWaitEvent(s->stream, s->ev_bnd, 0));
     s->bnd_pending = 0;
+    if (s->bnd_mode == 3) ws = s->bnd;
   }
   int sides = 0;
   WaitArgs w;
@@ -3924,10 +3942,10 @@ int pft_slab_halo_wait(pft_slab* s, unsigned long long seq)
   if (s->wait_streamops) {
     // A/B (PFT_WAIT_STREAMOPS=1): the runtime's stream waits, then a separate receive launch
     for (int side = 0; side < 2; ++side)
-      if (s->peer[side].on) HIPCHK(hipStreamWaitValue64(s->stream, s->sig + side, seq, hipStreamWaitValueGte, ~0ULL));
-    if (sides) halo_recv_kernel<<<blocks, 256, 0, s->stream>>>(w.r);
+      if (s->peer[side].on) HIPCHK(hipStreamWaitValue64(ws, s->sig + side, seq, hipStreamWaitValueGte, ~0ULL));
+    if (sides) halo_recv_kernel<<<blocks, 256, 0, ws>>>(w.r);
   } else {
-    halo_wait_kernel<<<blocks, 256, 0, s->stream>>>(w);
+    halo_wait_kernel<<<blocks, 256, 0, ws>>>(w);
   }
   HIPCHK(hipGetLastError());
   return 0;

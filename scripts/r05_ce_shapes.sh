@@ -8,7 +8,7 @@ mkdir -p $OUT
 for rep in ${REPS:-1}; do
   for dom in "400 0.06,0.06,0.015 n8" "318 0.06,0.06,0.03 n4" "252 0.06,0.06,0.06 n2"; do
     set -- $dom
-    for v in ${VARS:-ipc 0 2}; do
+    for v in ${VARS:-ipc 0 2 3}; do
       args="--steps 100 --no-cpu --grid-nodes $1 --domain $2 --self-exchange"
       if [ $v = ipc ]; then
         timeout -k 10 300 python bench.py $args --transport ipc > $OUT/$3_${v}_$rep.json 2>>$OUT/err.log

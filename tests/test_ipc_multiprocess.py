@@ -211,8 +211,10 @@ def test_lost_ipc_halo_ends_in_device_error_not_a_hang(tmp_path):
 
 # copy-engine options (pft_slab_set_boundary_stream): by default the pair kernels' boundary launch
 # runs beside their interior launch (PFT_CE_BND 2); 0: every boundary launch before its interior,
-# 1: every one beside
+# 1: every one beside; 3: the boundary pipeline (every one beside, the halo waits on the boundary
+# stream: no interior launch waits for a neighbour)
 _SERIAL = {"PFT_CE_BND": "0"}
+_PIPE = {"PFT_CE_BND": "3"}
 _BESIDE_ALL = {"PFT_CE_BND": "1"}
 
 
@@ -222,7 +224,10 @@ _BESIDE_ALL = {"PFT_CE_BND": "1"}
                                                               (3, 2, 1, (0, 1, 2), {"PFT_CE_SEQTAB": "5"}),
                                                               (2, 2, 0, (0, 1), _SERIAL), (3, 2, 1, (0, 1, 2), _SERIAL),
                                                               (3, 0, 0, (0, 1, 2), _BESIDE_ALL),
-                                                              (3, 2, 1, (0, 2), _BESIDE_ALL)])
+                                                              (3, 2, 1, (0, 2), _BESIDE_ALL),
+                                                              (3, 2, 0, (0, 1, 2), _PIPE), (3, 2, 1, (0, 1, 2), _PIPE),
+                                                              (3, 0, 1, (0, 1, 2), _PIPE), (3, 2, 1, (1,), _PIPE),
+                                                              (2, 2, 0, (0, 1), dict(_PIPE, PFT_CE_SEQTAB="3"))])
 def test_g20_processes_copy_engine_equal_reference(tmp_path, nranks, pair, staged, ce_ranks, xenv):
     """the boundary planes first, their exchange as SDMA copies and 8-byte flag copies on the comm
     stream beside the interior launch, the receiver's flag wait before the next launch: golden g20
@@ -249,7 +254,7 @@ def test_g20_processes_copy_engine_equal_reference(tmp_path, nranks, pair, stage
         assert np.array_equal(full, A[f"traj_m0_state{i}"])
 
 
-@pytest.mark.parametrize("staged,xenv", [(0, {}), (1, {}), (0, _SERIAL), (1, _SERIAL)])
+@pytest.mark.parametrize("staged,xenv", [(0, {}), (1, {}), (0, _SERIAL), (1, _SERIAL), (0, _PIPE), (1, _PIPE)])
 def test_400_processes_copy_engine_equal_one_slab(tmp_path, staged, xenv):
     """400^3 over 2 processes with the pair kernels, the exchange on the copy engines"""
     steps = 10
@@ -269,7 +274,7 @@ def test_400_processes_copy_engine_equal_one_slab(tmp_path, staged, xenv):
     assert np.array_equal(np.concatenate([r["states"][0] for r in res], axis=1), x)
 
 
-@pytest.mark.parametrize("xenv", [{}, _SERIAL, _BESIDE_ALL])
+@pytest.mark.parametrize("xenv", [{}, _SERIAL, _BESIDE_ALL, _PIPE])
 @pytest.mark.parametrize("staged", [0, 1])
 @pytest.mark.parametrize("pair", [2, 0])
 def test_ipc_copy_engine_self_exchange_equals_reference(pair, staged, xenv, monkeypatch):
