@@ -1995,7 +1995,7 @@ struct pft_slab {
   // a launch of the boundary planes (PFT_K_BOUNDARY/2) runs on `bnd` beside the interior launch on
   // the compute stream instead of before it; the exchange waits for ev_bnd, and so does the compute
   // stream before the next launch (pft_slab_halo_wait).  bnd_mode 1: every boundary launch, 2: the
-  // pair kernels' (run_pair), 3: every one, with the halo waits on `bnd` (the boundary pipeline)
+  // pair kernels' (run_pair), 3: the pair kernels', with the halo waits on `bnd` (the boundary pipeline)
   int bnd_mode, bnd_pending, ce_streams;
   int ce_marked;         // pft_slab_halo_mark recorded ev_order[0] after the launch the next put_ce sends
   int wait_streamops;    // A/B: halo waits as hipStreamWaitValue64 (env PFT_WAIT_STREAMOPS=1)
@@ -2789,12 +2789,16 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   }
   dim3 g((unsigned)(a.ntile * a.nchunk));
   bool extra = false;
-  // a stage launch's interior fills the chip: its boundary runs beside it only in bnd_mode 1 and 3
-  // (3: the boundary pipeline, pft_slab_halo_wait)
-  const bool beside = bnd && (s->bnd_mode == 1 || s->bnd_mode == 3);
-  // the reduction of the previous error-norm launch's partials needs that launch complete: in the
-  // pipeline a boundary launch may run beside its end, so the interior launch takes it
-  if (stage == 1 && kind == KFUSED && s->defer_n > 0 && !(beside && s->bnd_mode == 3)) {
+  // a stage launch's interior fills the chip: its boundary runs beside it only in bnd_mode 1 (slower:
+  // the two launches' workgroups are dealt interleaved and the interior ends late).  In the boundary
+  // pipeline (bnd_mode 3) the halo waits are on the boundary stream: a stage launch's boundary on
+  // the compute stream first joins it
+  const bool beside = bnd && s->bnd_mode == 1;
+  if (bnd && s->bnd_mode == 3 && s->bnd) {
+    HIPCHK(hipEventRecord(s->ev_join, s->bnd));
+    HIPCHK(hipStreamWaitEvent(s->stream, s->ev_join, 0));
+  }
+  if (stage == 1 && kind == KFUSED && s->defer_n > 0) {
     // the previous error-norm launch's partials: reduced and published by one extra workgroup
     a.part = s->part;
     a.npart = s->defer_n;
@@ -3862,8 +3866,8 @@ int pft_slab_set_boundary_stream(pft_slab* s, int on)
   if (on && !s->ev_copy) HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
   // bnd_mode 2 (default): the pair kernels' boundary launch on its own stream beside their interior
   // launch (run_pair); a stage launch's boundary runs before its interior.  3: the boundary
-  // pipeline -- every boundary launch beside its interior, and the halo waits on the boundary
-  // stream (pft_slab_halo_wait), so that no interior launch waits for a neighbour's flag.  Env overrides for A/B (profiles/r05_ce_ab.txt): PFT_CE_BND=0 every
+  // pipeline -- as 2, and the halo waits on the boundary stream (pft_slab_halo_wait), so that no
+  // pair interior launch waits for a neighbour's flag.  Env overrides for A/B (profiles/r05_ce_ab.txt): PFT_CE_BND=0 every
   // boundary before its interior, 1 every one beside (slower: a stage launch's interior fills the
   // chip, the two launches' workgroups are dealt interleaved and the boundary ends late,
   // profiles/r05_ce_trace_bnd.txt); PFT_CE_STREAMS=1 puts every copy on the comm stream (slower)

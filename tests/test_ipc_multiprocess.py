@@ -211,8 +211,8 @@ def test_lost_ipc_halo_ends_in_device_error_not_a_hang(tmp_path):
 
 # copy-engine options (pft_slab_set_boundary_stream): by default the pair kernels' boundary launch
 # runs beside their interior launch (PFT_CE_BND 2); 0: every boundary launch before its interior,
-# 1: every one beside; 3: the boundary pipeline (every one beside, the halo waits on the boundary
-# stream: no interior launch waits for a neighbour)
+# 1: every one beside; 3: the boundary pipeline (as 2, the halo waits on the boundary
+# stream: no pair interior launch waits for a neighbour)
 _SERIAL = {"PFT_CE_BND": "0"}
 _PIPE = {"PFT_CE_BND": "3"}
 _BESIDE_ALL = {"PFT_CE_BND": "1"}
