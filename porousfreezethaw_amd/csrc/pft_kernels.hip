@@ -3864,16 +3864,19 @@ int pft_slab_set_boundary_stream(pft_slab* s, int on)
     HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
   }
   if (on && !s->ev_copy) HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
-  // bnd_mode 2 (default): the pair kernels' boundary launch on its own stream beside their interior
-  // launch (run_pair); a stage launch's boundary runs before its interior.  3: the boundary
+  // bnd_mode 2: the pair kernels' boundary launch on its own stream beside their interior launch
+  // (run_pair); a stage launch's boundary runs before its interior.  3 (default): the boundary
   // pipeline -- as 2, and the halo waits on the boundary stream (pft_slab_halo_wait), so that no
-  // pair interior launch waits for a neighbour's flag.  Env overrides for A/B (profiles/r05_ce_ab.txt): PFT_CE_BND=0 every
-  // boundary before its interior, 1 every one beside (slower: a stage launch's interior fills the
-  // chip, the two launches' workgroups are dealt interleaved and the boundary ends late,
-  // profiles/r05_ce_trace_bnd.txt); PFT_CE_STREAMS=1 puts every copy on the comm stream (slower)
+  // pair interior launch waits for a neighbour's flag: a late copy delays only the next boundary
+  // launch, which has the interior's length of slack (profiles/r05_ce_shapes.txt: +1% over 2 on
+  // one GPU).  Env overrides for A/B (profiles/r05_ce_ab.txt, r05_ce_shapes.txt): PFT_CE_BND=2 the
+  // waits on the compute stream, 0 every boundary before its interior, 1 every one beside (slower:
+  // a stage launch's interior fills the chip, the two launches' workgroups are dealt interleaved
+  // and the boundary ends late, profiles/r05_ce_trace_bnd.txt); PFT_CE_STREAMS=1 puts every copy
+  // on the comm stream (slower)
   const char* eb = getenv("PFT_CE_BND");
   const char* es = getenv("PFT_CE_STREAMS");
-  s->bnd_mode = !on ? 0 : eb && atoi(eb) >= 0 && atoi(eb) <= 3 ? atoi(eb) : 2;
+  s->bnd_mode = !on ? 0 : eb && atoi(eb) >= 0 && atoi(eb) <= 3 ? atoi(eb) : 3;
   s->ce_streams = es && atoi(es) == 1 ? 1 : 2;
   if (s->ce_streams == 2 && !s->ev_copy) HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
   if (!s->ev_side) HIPCHK(hipEventCreateWithFlags(&s->ev_side, hipEventDisableTiming));

@@ -209,12 +209,12 @@ def test_lost_ipc_halo_ends_in_device_error_not_a_hang(tmp_path):
 
 # ---- the exchange on the copy engines (PFT_IPC_CE=1: pft_slab_halo_put_ce) --------------------
 
-# copy-engine options (pft_slab_set_boundary_stream): by default the pair kernels' boundary launch
-# runs beside their interior launch (PFT_CE_BND 2); 0: every boundary launch before its interior,
-# 1: every one beside; 3: the boundary pipeline (as 2, the halo waits on the boundary
-# stream: no pair interior launch waits for a neighbour)
+# copy-engine options (pft_slab_set_boundary_stream): by default the boundary pipeline (PFT_CE_BND 3:
+# the pair kernels' boundary launch beside their interior launch, the halo waits on the boundary
+# stream, so no pair interior launch waits for a neighbour); 2: the same with the waits on the
+# compute stream; 0: every boundary launch before its interior; 1: every one beside
 _SERIAL = {"PFT_CE_BND": "0"}
-_PIPE = {"PFT_CE_BND": "3"}
+_PIPE = {"PFT_CE_BND": "2"}
 _BESIDE_ALL = {"PFT_CE_BND": "1"}
 
 
