@@ -150,6 +150,11 @@ def main():
     dist = None
     comm = None
     if world > 1:
+        # a neighbour that never delivers ends the run within a minute (every wait polls; the
+        # library's default bound is 300 s), so that a failed first exchange falls back to RCCL and
+        # a failure in the timed region exits non-zero before the driver's own limit
+        os.environ.setdefault("PFT_IPC_TIMEOUT", "60")
+        os.environ.setdefault("PFT_COMM_TIMEOUT", "60")
         # torch.distributed (gloo, host only) is the rendezvous and the barrier; the data path is
         # libpft's communicator (pft_comm.h).  torch never touches the GPU here.
         import torch.distributed as dist
