@@ -1998,6 +1998,7 @@ struct pft_slab {
   // pair kernels' (run_pair), 3: the pair kernels', with the halo waits on `bnd` (the boundary pipeline)
   int bnd_mode, bnd_pending, ce_streams;
   int ce_marked;         // pft_slab_halo_mark recorded ev_order[0] after the launch the next put_ce sends
+  int bnd_split;         // the exchange's boundary launch ran before its interior on the compute stream
   int wait_streamops;    // A/B: halo waits as hipStreamWaitValue64 (env PFT_WAIT_STREAMOPS=1)
   hipStream_t bnd;
   hipEvent_t ev_bnd, ev_pre, ev_copy, ev_side, ev_join;
@@ -2840,6 +2841,8 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   if (beside) {
     HIPCHK(hipEventRecord(s->ev_bnd, s->bnd));
     s->bnd_pending = 1;
+  } else if (bnd) {
+    s->bnd_split = 1;   // a boundary launch before its interior on the compute stream
   }
   return 0;
 }
@@ -3911,7 +3914,12 @@ int pft_slab_halo_wait(pft_slab* s, unsigned long long seq)
     HIPCHK(hipStreamWaitEvent(s->stream, s->ev_bnd, 0));
     s->bnd_pending = 0;
     if (s->bnd_mode == 3) ws = s->bnd;
+  } else if (s->bnd_split && s->bnd_mode == 3 && s->bnd) {
+    // a boundary launch before its interior (stage 1): its flags too are waited for on the
+    // boundary stream, which the next boundary launch follows (run_pair beside, run_stage joins)
+    ws = s->bnd;
   }
+  s->bnd_split = 0;
   int sides = 0;
   WaitArgs w;
   memset(&w, 0, sizeof(w));
