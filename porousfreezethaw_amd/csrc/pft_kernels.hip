@@ -3953,6 +3953,10 @@ int pft_slab_halo_wait(pft_slab* s, unsigned long long seq)
     // flag -- it would wait out PFT_IPC_TIMEOUT.  A few blocks then, which copy more each.
     for (int side = 0; side < 2; ++side)
       if (((sides >> side) & 1) && !s->peer[side].remote) blocks = std::min(blocks, 32);
+    // in the boundary pipeline the wait runs beside an interior launch and the next one does not
+    // wait for it: its blocks must not hold the CUs that launch's workgroups need (128 blocks of 4
+    // waves: 16 CUs' worth; the 20 MB of the receive still take ~10 us)
+    if (ws == s->bnd) blocks = std::min(blocks, 128);
   }
   if (s->wait_streamops) {
     // A/B (PFT_WAIT_STREAMOPS=1): the runtime's stream waits, then a separate receive launch
