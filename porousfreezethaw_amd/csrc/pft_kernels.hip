@@ -3913,10 +3913,7 @@ int pft_slab_halo_wait(pft_slab* s, unsigned long long seq)
     // the boundary launch ran beside the interior one: its planes are the next launch's input
     HIPCHK(hipStreamWaitEvent(s->stream, s->ev_bnd, 0));
     s->bnd_pending = 0;
-    // ... except x(t+h)'s: the next step's stage 1 reads it first, with its boundary launch before
-    // its interior on the compute stream -- which would only join the boundary stream's wait (a
-    // cross-stream hop of ~9 us where a kernel on the compute stream costs ~6)
-    if (s->bnd_mode == 3 && s->put_role != PFT_BUF_XN) ws = s->bnd;
+    if (s->bnd_mode == 3) ws = s->bnd;
   } else if (s->bnd_split && s->bnd_mode == 3 && s->bnd) {
     // a boundary launch before its interior (stage 1): its flags too are waited for on the
     // boundary stream, which the next boundary launch follows (run_pair beside, run_stage joins)
