@@ -3801,6 +3801,14 @@ int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsign
     unsigned long long* h = s->seqhost + (size_t)s->seq_half * PFT_SEQTAB;
     for (int i = 0; i < NSEQ; ++i) h[i] = s->seq_base + 1 + i;
     HIPCHK(hipMemcpyAsync(s->seqtab, h, sizeof(unsigned long long) * NSEQ, hipMemcpyHostToDevice, s->comm));
+    if (s->ce_streams != 1) {
+      // the side stream's flag copies read the new table: this exchange's (and so every later one's)
+      // follow the refill.  (An event on every exchange instead held each side flag behind the comm
+      // stream's copies and put a marker between the comm stream's last copy and its flag: ~10-20
+      // us later flags, profiles/r05_ce_trace_pipe.txt.)
+      HIPCHK(hipEventRecord(s->ev_copy, s->comm));
+      HIPCHK(hipStreamWaitEvent(s->side, s->ev_copy, 0));
+    }
   }
   // the planes to the neighbour below go on the comm stream, to the one above on the side stream
   // (two copy engines; ce_streams = 1: all on the comm stream), each followed by its neighbour's
@@ -3838,11 +3846,6 @@ int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsign
     }
   }
   const unsigned long long* sv = s->seqtab + (seq - 1 - s->seq_base);
-  if (cs[1] != cs[0]) {
-    // the table refill above is on the comm stream: the side stream's flag copy follows it
-    HIPCHK(hipEventRecord(s->ev_copy, s->comm));
-    HIPCHK(hipStreamWaitEvent(cs[1], s->ev_copy, 0));
-  }
   if (s->peer[0].on) HIPCHK(hipMemcpyAsync(s->peer[0].sig + 1, sv, 8, hipMemcpyDeviceToDeviceNoCU, cs[0]));
   if (s->peer[1].on) HIPCHK(hipMemcpyAsync(s->peer[1].sig + 0, sv, 8, hipMemcpyDeviceToDeviceNoCU, cs[1]));
   return 0;
