@@ -32,6 +32,7 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
+PROBE_STEPS = 3    # attempted steps of the N > 1 setup's delivery check (bench.py main)
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
@@ -185,6 +186,7 @@ def main():
                             gl_static=a.gl_static, kz=a.kz or None, tile=a.tile,
                             recompute=not a.no_recompute, device_ic=not a.host_ic)
 
+    probe_calls = []   # solve calls made by the setup's check (world > 1), replayed by the parity re-run
     if world > 1:
         # The first exchanges (the device IC's ghost planes) run inside the setup.  If the ipc transport
         # the run chose by itself fails there on any rank (mapping a neighbour's buffers across GPUs,
@@ -198,6 +200,15 @@ def main():
             # check after the timed region)
             if not a.host_ic and not halo_delivered(L, sim, dist, world, rank):
                 raise RuntimeError("the ghost planes after the setup exchange differ from the neighbours' planes")
+            if not a.host_ic and transport_auto and a.transport in ("ipc", "ipc-ce"):
+                # the same after a few attempted steps: the split launches' exchanges (copy engines,
+                # boundary stream) -- the first solve call, replayed by the parity re-run like the rest
+                rc = sim.solve_ex(base["final_time"], PROBE_STEPS, P.PFT_SOLVE_KEEP_DEVICE)
+                probe_calls.append(PROBE_STEPS)
+                delivered = halo_delivered(L, sim, dist, world, rank)   # collective: every rank calls it
+                if rc != 2 or not delivered:
+                    raise RuntimeError(f"after {PROBE_STEPS} attempted steps (rc {rc}) the ghost planes differ "
+                                       f"from the neighbours' planes")
         except Exception as e:  # noqa: BLE001
             print(f"rank {rank}: setup over {a.transport} failed: {e}", file=sys.stderr)
             fail = 1
@@ -217,6 +228,7 @@ def main():
             print(f"rank {rank}: every rank falls back to RCCL", file=sys.stderr)
             comm, a.transport = make_comm(L, "rccl", world, rank, dev, dist, fallback=False)
             sim = make_sim()
+            probe_calls = []
     else:
         sim = make_sim()
     init_s = time.time() - t0
@@ -239,7 +251,7 @@ def main():
     # measured 15 853-16 090 where the steady state is 17 592.  Untimed attempted steps of the same
     # solve run until --prewarm-s has passed (every rank takes the same decision: the max over
     # ranks); they are solve calls like the warm-up, replayed by the N > 1 parity re-run.
-    calls = []                                 # the capped solve calls, in order (the parity re-run repeats them)
+    calls = list(probe_calls)                  # the capped solve calls, in order (the parity re-run repeats them)
     prewarm_steps = 0
     tp = time.perf_counter()
     while a.prewarm_s > 0 and prewarm_steps < 5000:
