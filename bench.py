@@ -200,7 +200,7 @@ def main():
             # check after the timed region)
             if not a.host_ic and not halo_delivered(L, sim, dist, world, rank):
                 raise RuntimeError("the ghost planes after the setup exchange differ from the neighbours' planes")
-            if not a.host_ic and transport_auto and a.transport in ("ipc", "ipc-ce"):
+            if not a.host_ic and a.transport in ("ipc", "ipc-ce"):
                 # the same after a few attempted steps: the split launches' exchanges (copy engines,
                 # boundary stream) -- the first solve call, replayed by the parity re-run like the rest
                 rc = sim.solve_ex(base["final_time"], PROBE_STEPS, P.PFT_SOLVE_KEEP_DEVICE)
