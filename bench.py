@@ -70,8 +70,11 @@ def parse():
                     help="before the W counted warm-up steps, run untimed attempted steps for about this "
                          "long so the GPU clock has left its idle level (0: off; DESIGN 5)")
     ap.add_argument("--grid-nodes", type=int, default=400, help="grid_nodes G of the 1-GPU case")
-    ap.add_argument("--shape", choices=("cube", "tall"), default="cube",
-                    help="N>1 weak-scaling family (module docstring)")
+    ap.add_argument("--shape", choices=("cube", "tall", "strong"), default="cube",
+                    help="N>1 workload family (module docstring): cube/tall weak scaling; strong = the "
+                         "--grid-nodes grid itself split N ways (BASELINE configs[3]: 400^3 4-way)")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="N>1: skip the strong-split sub-run (config.strong)")
     ap.add_argument("--literal-cube", action="store_true",
                     help="L1 = L2 = L3 = 0.06 m: G x G x G cells (SURVEY 8(d) secondary number)")
     ap.add_argument("--domain", default=None,
@@ -123,6 +126,12 @@ def parse():
 
 def main():
     a = parse()
+    worker = os.environ.get("PFT_BENCH_WORKER") == "1"
+    if not worker and (a.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1") or 1) > 1):
+        # N > 1: this process only launches and watches the ranks (supervise); it never loads libpft
+        sys.exit(supervise(a))
+    if worker and os.environ.get("PFT_BENCH_DRYRUN") == "1":
+        sys.exit(dryrun_worker(a))
     # stdout carries exactly one JSON line: anything else written to fd 1 (RCCL's version banner
     # at communicator init, library diagnostics) goes to stderr
     json_fd = os.dup(1)
@@ -380,12 +389,12 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(el / steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if (a.shape == "strong" and world > 1) else "weak",
         "vs_baseline": vs_base,
         "dtype": "f64",
         "data": "synthetic: default Params initial condition (u=293.15 K, ice cap, glass walls, "
                 "200 glass beads from the reference's data file), t=0, h=tau=1",
-        "config": {"workload": (f"{gn}^3 default Params" if a.shape == "cube" or world == 1 else
+        "config": {"workload": (f"{gn}^3 default Params" if a.shape in ("cube", "strong") or world == 1 else
                                 f"{a.grid_nodes}^3 slab x {world} (tall)") +
                                f": {n1}x{n2}x{total_n3} cells, Z-slab split {world}-way "
                                f"({n1}x{n2}x{sim.grid.n3} on rank {rank})",
@@ -451,7 +460,205 @@ def main():
     if dist is not None:
         dist.destroy_process_group()
     if not ok:
-        sys.exit(f"parity: the {world}-slab run differs from the single-slab run of the same steps")
+        print(f"parity: the {world}-slab run differs from the single-slab run of the same steps", file=sys.stderr)
+        sys.exit(PARITY_EXIT)
+
+
+# ---- N > 1: the ranks as child processes of a supervisor ------------------------------------
+# `bench.py --gpus N` started as ONE process (no RANK / WORLD_SIZE) spawns the N ranks itself;
+# started by torch.distributed.run, each of its N processes supervises one rank.  Either way the
+# ranks are fresh child processes (PFT_BENCH_WORKER=1) with their own rendezvous port, and the
+# supervisors never load libpft or touch a GPU.  That buys two things:
+#   - the run cannot fail for launch reasons: a plain `python bench.py --gpus 4` measures;
+#   - a failed attempt is retried in FRESH processes: when the transport is auto (ipc-ce across
+#     GPUs, ipc when ranks share one) or ipc-ce and any rank fails -- an exchange that never
+#     arrives (the bounded waits end it), a device error, a parity mismatch -- every rank is
+#     started again over RCCL.  The JSON line records every attempt ("launch").
+# With N > 1 a second set of ranks then times the reference's 400^3 grid split N ways (BASELINE
+# configs[3] at N = 4: 200 x 200 x 100 per rank) with its own parity re-run: config.strong.
+PARITY_EXIT = 3
+
+
+def _child_env(rank, local, world, port, transport):
+    # (not torch.distributed.run's agent store: the ranks rendezvous on their own port)
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    env.update(PFT_BENCH_WORKER="1", RANK=str(rank), LOCAL_RANK=str(local), WORLD_SIZE=str(world),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    env.setdefault("LOCAL_WORLD_SIZE", str(world))
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["PFT_BENCH_ATTEMPT_TRANSPORT"] = transport
+    return env
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_children(specs, timeout_s, grace_s=30.0):
+    """start the child ranks (argv, env, capture_stdout) and wait for all of them; once one has
+    failed, the others get grace_s to end by themselves (a failed rank closes its gloo sockets, which
+    ends its peers' collectives) before they are killed, as is every child still running after
+    timeout_s.  Returns (exit codes, captured stdout of the capturing child)."""
+    import subprocess
+    procs = []
+    for argv, env, cap in specs:
+        procs.append(subprocess.Popen(argv, env=env, stdout=subprocess.PIPE if cap else sys.stderr,
+                                      stderr=None, start_new_session=True))
+    out = {}
+    import threading
+
+    def drain(i, p):
+        out[i] = p.stdout.read()
+
+    readers = [threading.Thread(target=drain, args=(i, p), daemon=True) for i, p in enumerate(procs) if p.stdout]
+    for t in readers:
+        t.start()
+    t0 = time.time()
+    failed_at = None
+    while True:
+        codes = [p.poll() for p in procs]
+        if all(c is not None for c in codes):
+            break
+        if failed_at is None and any(c not in (None, 0) for c in codes):
+            failed_at = time.time()
+        now = time.time()
+        if now - t0 > timeout_s or (failed_at is not None and now - failed_at > grace_s):
+            for p in procs:
+                if p.poll() is None:
+                    print(f"bench supervisor: killing rank process {p.pid} "
+                          f"({'time limit' if now - t0 > timeout_s else 'a peer failed'})", file=sys.stderr)
+                    try:
+                        os.killpg(p.pid, 9)
+                    except OSError:
+                        pass
+            for p in procs:
+                p.wait()
+            break
+        time.sleep(0.2)
+    for t in readers:
+        t.join(timeout=10)
+    codes = [p.returncode for p in procs]
+    cap = next((out.get(i, b"") for i, (argv, env, c) in enumerate(specs) if c), b"")
+    return codes, cap.decode(errors="replace")
+
+
+def _last_json(text):
+    for line in reversed(text.strip().splitlines()):
+        try:
+            return json.loads(line)
+        except ValueError:
+            continue
+    return None
+
+
+def supervise(a):
+    """the N > 1 launcher (comment block above): returns the process exit code"""
+    world_env = int(os.environ.get("WORLD_SIZE", "1") or 1)
+    launched = world_env > 1                  # torch.distributed.run: one supervisor per rank
+    world = world_env if launched else a.gpus
+    rank = int(os.environ.get("RANK", "0")) if launched else 0
+    local = int(os.environ.get("LOCAL_RANK", str(rank))) if launched else 0
+    dist = None
+    if launched:
+        import torch.distributed as dist      # gloo: host only, the supervisors' own rendezvous
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    script = [sys.executable, "-u", os.path.abspath(__file__)]
+    argv0 = [x for x in sys.argv[1:]]
+    timeout_s = float(os.environ.get("PFT_BENCH_CHILD_TIMEOUT", "1200"))
+
+    def attempt(extra):
+        """one set of N child ranks with these extra arguments: (every rank ok, rank 0's JSON, codes)"""
+        port = [_free_port() if rank == 0 else 0]
+        if dist is not None:
+            dist.broadcast_object_list(port, src=0)
+        tr = extra[extra.index("--transport") + 1] if "--transport" in extra else a.transport
+        if launched:
+            specs = [(script + argv0 + extra, _child_env(rank, local, world, port[0], tr), rank == 0)]
+        else:
+            specs = [(script + argv0 + extra, _child_env(r, r, world, port[0], tr), r == 0) for r in range(world)]
+        codes, text = _run_children(specs, timeout_s)
+        if dist is not None:
+            allc = [None] * world
+            dist.all_gather_object(allc, codes[0])
+            codes = allc
+        line = _last_json(text) if rank == 0 else None
+        ok = all(c == 0 for c in codes) and (rank != 0 or line is not None)
+        if dist is not None:
+            import torch
+            t = torch.tensor([0 if ok else 1], dtype=torch.int64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ok = not int(t.item())
+        print(f"bench supervisor (rank {rank}): {' '.join(extra) or 'as given'}: rank exit codes {codes}", file=sys.stderr)
+        return ok, line, codes
+
+    plans = [a.transport] + (["rccl"] if a.transport in ("auto", "ipc-ce") else [])
+    attempts, out, success = [], None, False
+    for tr in plans:
+        ok, line, codes = attempt(["--transport", tr])
+        attempts.append({"transport": tr, "exit_codes": codes, "ok": ok})
+        if ok:
+            out, success = line, True        # (every rank agrees on ok; only rank 0 has the line)
+            break
+        if tr != plans[-1]:
+            print(f"bench supervisor (rank {rank}): the run over '{tr}' failed on a rank; every rank starts again "
+                  f"over RCCL in fresh processes", file=sys.stderr)
+    strong = None
+    if success and world > 1 and not a.no_strong and a.shape != "strong" and not a.self_exchange:
+        # BASELINE configs[3] (at N = 4): the 400^3 grid split N ways, over the transport the main run used
+        tr = (out or {}).get("config", {}).get("transport") or "auto" if rank == 0 else "auto"
+        trl = [tr]
+        if dist is not None:
+            dist.broadcast_object_list(trl, src=0)
+        sok, sline, scodes = attempt(["--transport", trl[0], "--shape", "strong", "--no-cpu"])
+        if rank == 0:
+            if sok and sline:
+                c = sline.get("config", {})
+                strong = {"workload": c.get("workload"), "scaling": "strong", "value": sline.get("value"),
+                          "unit": sline.get("unit"), "ms_per_step": sline.get("ms_per_step"),
+                          "steps": sline.get("steps"), "cells": c.get("cells"), "transport": c.get("transport"),
+                          "parity": sline.get("parity"), "roofline": sline.get("roofline")}
+            else:
+                strong = {"error": f"the strong-split run failed (rank exit codes {scodes})"}
+    if dist is not None:
+        dist.destroy_process_group()
+    if rank != 0:
+        return 0 if success else 1
+    if out is None:
+        print(f"bench supervisor: no attempt succeeded: {attempts}", file=sys.stderr)
+        return 1
+    out["launch"] = {"mode": "torchrun (one supervisor per rank, one child rank each)" if launched
+                     else "self-spawn (one supervisor, N child ranks)", "attempts": attempts}
+    if strong is not None:
+        out.setdefault("config", {})["strong"] = strong
+    sys.stdout.write(json.dumps(out) + "\n")
+    sys.stdout.flush()
+    return 0
+
+
+def dryrun_worker(a):
+    """test hook (PFT_BENCH_DRYRUN=1, tests/test_bench_launch.py): a child rank that does the
+    rendezvous and a barrier and prints a stand-in line, without a GPU.  PFT_BENCH_DRYRUN_FAIL =
+    "<rank>:<transport>" makes that rank exit non-zero when its attempt uses that transport."""
+    import torch.distributed as dist
+    world = int(os.environ["WORLD_SIZE"])
+    rank = int(os.environ["RANK"])
+    tr = os.environ.get("PFT_BENCH_ATTEMPT_TRANSPORT", a.transport)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    fail = os.environ.get("PFT_BENCH_DRYRUN_FAIL", "")
+    if fail and fail.split(":")[0] == str(rank) and fail.split(":")[1] == tr:
+        print(f"dryrun rank {rank}: failing on purpose over {tr}", file=sys.stderr)
+        os._exit(5)
+    names = [None] * world
+    dist.all_gather_object(names, {"rank": rank, "pid": os.getpid(), "local": int(os.environ.get("LOCAL_RANK", "-1"))})
+    dist.barrier()
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": 0.0, "dryrun": True, "n_gpus": world,
+                          "config": {"transport": tr, "shape": a.shape, "ranks": names}}))
+    dist.destroy_process_group()
+    return 0
 
 
 def halo_delivered(L, sim, dist, world, rank):
@@ -614,6 +821,10 @@ def workload(grid_nodes, world, shape="cube", literal_cube=False, mode=0, domain
     Lc = (PR.float_val("0.06"),) * 3 if literal_cube else None
     if domain:
         Lc = tuple(PR.float_val(v) for v in domain.split(","))
+    if shape == "strong":
+        # the grid itself, its n3 planes split over the ranks (intertrack.c:1776-1800)
+        base = PR.default_params(grid_nodes=grid_nodes, calc_mode=mode, L=Lc)
+        return grid_nodes, base, (base["n1"], base["n2"], base["n3"]), (base["L1"], base["L2"], base["L3"])
     if shape == "cube" and world > 1:
         gn = int(round(grid_nodes * world ** (1.0 / 3.0) / 4.0)) * 4
         base = PR.default_params(grid_nodes=gn, calc_mode=mode, L=Lc)

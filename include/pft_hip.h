@@ -60,6 +60,13 @@ int pft_hip_get_device(int * dev);
 /* the GPU's PCI location (domain, bus, device) as one integer: equal across processes exactly when
    they use the same physical GPU (the ipc transport's staged-or-direct decision) */
 int pft_hip_device_phys_id(int dev, int * id);
+/* the GPU's full identity as text: its PCI bus id string with the function (hipDeviceGetPCIBusId)
+   and its UUID (hipDeviceGetUuid), "dddd:bb:dd.f/<32 hex digits>".  Two processes use the same GPU
+   -- the same L2s -- only when the strings are equal: partitions of one package (several HIP devices
+   at one bus:device) differ in the function or the UUID, and the ipc transport stages its receive
+   between them (pft_slab_ipc_set_peer).  len >= PFT_DEV_IDENT_BYTES. */
+#define PFT_DEV_IDENT_BYTES 80
+int pft_hip_device_ident(int dev, char * buf, int len);
 int pft_hip_device_sync(void);
 const char * pft_hip_last_error(void);
 
@@ -272,11 +279,18 @@ int pft_probe_copy(double * dst, const double * src, size_t n, void * stream);
 int pft_slab_ipc_export(pft_slab * s, void * handles);
 /* 1 when this process asks for staged receive between processes on one GPU (env PFT_IPC_STAGED=1) */
 int pft_ipc_staged_env(void);
-/* peer_staged: the neighbour's own staged-receive choice (its PFT_IPC_STAGED, published at attach);
-   both ends of a link stage when either asks for it, or when the neighbour is on another GPU */
-int pft_slab_ipc_set_peer(pft_slab * s, int side, const void * handles, int n3, long fs, int device,
+/* remote: 1 unless the neighbour provably uses this process's GPU (equal pft_hip_device_ident);
+   peer_staged: the neighbour's own staged-receive choice (its PFT_IPC_STAGED, published at attach);
+   both ends of a link stage when either asks for it, or when the neighbour is remote */
+int pft_slab_ipc_set_peer(pft_slab * s, int side, const void * handles, int n3, long fs, int remote,
                           int peer_staged);
 int pft_slab_ipc_close(pft_slab * s);
+/* how many ranks of the communicator use this slab's GPU (ipc attach, from the identities) */
+int pft_slab_set_gpu_ranks(pft_slab * s, int n);
+/* workgroups of a staged receive's wait launch (n doubles): every block spins on the neighbours'
+   flags first, so the count bounds the CUs a wait holds -- 32 with a staged neighbour on this GPU or
+   any other rank sharing it, 128 beside an interior launch, else up to 1024 */
+int pft_halo_wait_blocks(long n, int local_staged, int gpu_ranks, int on_boundary_stream);
 int pft_slab_halo_put(pft_slab * s, int role, int f0, int f1, unsigned long long seq);
 /* the same with deep = 1: also planes 2 and n3-1 into the neighbours' far ghost planes (the pair
    kernels' two-plane halo) */

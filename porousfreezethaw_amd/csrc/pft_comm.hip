@@ -34,6 +34,7 @@ enum { KIND_SELF = 0, KIND_RCCL = 1, KIND_LOOP = 2, KIND_IPC = 3 };
 
 struct IpcSlot {              // one rank's slab, published at attach
   int n3, device;
+  char ident[PFT_DEV_IDENT_BYTES];   // its GPU's identity (pft_hip_device_ident)
   int staged;                 // its staged-receive request (PFT_IPC_STAGED): both ends of a link agree
   long fs;
   char handles[PFT_IPC_HANDLE_BYTES];
@@ -448,6 +449,15 @@ int pft_comm_set_current(pft_comm* c)
 }
 pft_comm* pft_comm_current(void) { return g_current; }
 
+// 1 unless the neighbour's GPU is provably ours (equal, non-empty identities): a remote neighbour
+// stages its halo through our uncached receive buffer (pft_slab_ipc_set_peer); symmetric, so both
+// ends of a link take the same decision
+static int ident_remote(const IpcSlot* me, const IpcSlot* peer)
+{
+  if (!me->ident[0] || !peer->ident[0]) return 1;
+  return strncmp(me->ident, peer->ident, sizeof(me->ident)) != 0 || me->device != peer->device;
+}
+
 static int ipc_attach(pft_comm* c, pft_slab* s)
 {
   // collective: every rank attaches / detaches its slab at the same point of the run
@@ -475,6 +485,10 @@ static int ipc_attach(pft_comm* c, pft_slab* s)
   // the GPU's physical id, not the index: ranks whose device numbering differs (HIP_VISIBLE_DEVICES
   // per rank) still see whether a neighbour shares their GPU (pft_slab_ipc_set_peer: staged or not)
   if (!lrc) lrc = pft_hip_device_phys_id(c->device, &me->device);
+  // ... and in full (PCI bus id with the function, and the UUID): a neighbour counts as on this
+  // GPU only when the two identities are equal -- partitions of one package share a bus:device
+  // but not the L2s, and a direct write into their ghost planes could be read stale
+  if (!lrc) lrc = pft_hip_device_ident(c->device, me->ident, (int)sizeof(me->ident));
   me->fs = (long)pft_slab_field_stride(s);
   me->staged = pft_ipc_staged_env();
   if ((rc = ipc_round(c, nullptr, lrc ? 1 : 0, nullptr, 0, &recs))) return rc;   // every slot is published
@@ -485,12 +499,19 @@ static int ipc_attach(pft_comm* c, pft_slab* s)
   } else {
     if (c->rank > 0) {
       const IpcSlot* b = &c->shm->slot[c->rank - 1];
-      lrc = pft_slab_ipc_set_peer(s, 0, b->handles, b->n3, b->fs, b->device, b->staged);
+      lrc = pft_slab_ipc_set_peer(s, 0, b->handles, b->n3, b->fs, ident_remote(me, b), b->staged);
     }
     if (!lrc && c->rank < c->size - 1) {
       const IpcSlot* a = &c->shm->slot[c->rank + 1];
-      lrc = pft_slab_ipc_set_peer(s, 1, a->handles, a->n3, a->fs, a->device, a->staged);
+      lrc = pft_slab_ipc_set_peer(s, 1, a->handles, a->n3, a->fs, ident_remote(me, a), a->staged);
     }
+  }
+  if (!lrc) {
+    // the ranks on this GPU (this one included): a staged wait spins in few blocks when it shares
+    // the GPU with another rank (pft_halo_wait_blocks)
+    int same = 0;
+    for (int q = 0; q < c->size; ++q) same += !ident_remote(me, &c->shm->slot[q]);
+    lrc = pft_slab_set_gpu_ranks(s, same > 0 ? same : 1);
   }
   if (!lrc) lrc = pft_slab_set_boundary_stream(s, c->ce);
   {

@@ -1991,6 +1991,14 @@ struct pft_slab {
   unsigned long long* seqhost;
   unsigned long long seq_base;
   int seq_half, seq_n;
+  hipEvent_t ev_seq[2];  // recorded after each refill's H2D copy from that pinned half: the host
+                         // rewrites a half only once the copy that read it last has run
+  // the flag behind the completed plane copies (pft_slab_halo_put_ce, ce_fence): per side an event
+  // after its plane copies and a flag stream that waits for it
+  int ce_fence;
+  int gpu_ranks;         // ranks of the communicator on this slab's GPU (ipc attach; 0/1: alone)
+  hipStream_t fstream[2];
+  hipEvent_t ev_planes[2];
   // boundary launches on their own stream (pft_slab_set_boundary_stream; the copy-engine exchange):
   // a launch of the boundary planes (PFT_K_BOUNDARY/2) runs on `bnd` beside the interior launch on
   // the compute stream instead of before it; the exchange waits for ev_bnd, and so does the compute
@@ -2231,6 +2239,18 @@ int pft_hip_device_phys_id(int dev, int* id)
   *id = ((dom & 0xffff) << 13) | ((bus & 0xff) << 5) | (pdev & 0x1f);
   return 0;
 }
+int pft_hip_device_ident(int dev, char* buf, int len)
+{
+  if (!buf || len < PFT_DEV_IDENT_BYTES) return -2;
+  char bus[32] = {0};
+  hipUUID u;
+  memset(&u, 0, sizeof(u));
+  HIPCHK(hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, dev));
+  HIPCHK(hipDeviceGetUuid(&u, dev));
+  int n = snprintf(buf, (size_t)len, "%s/", bus);
+  for (int i = 0; i < 16 && n < len - 2; ++i) n += snprintf(buf + n, (size_t)(len - n), "%02x", (unsigned char)u.bytes[i]);
+  return 0;
+}
 int pft_hip_device_sync(void)
 {
   HIPCHK(hipDeviceSynchronize());
@@ -2363,6 +2383,11 @@ int pft_slab_destroy(pft_slab* s)
   if (s->ev_copy) (void)hipEventDestroy(s->ev_copy);
   if (s->ev_side) (void)hipEventDestroy(s->ev_side);
   if (s->ev_join) (void)hipEventDestroy(s->ev_join);
+  for (int i = 0; i < 2; ++i) {
+    if (s->ev_seq[i]) (void)hipEventDestroy(s->ev_seq[i]);
+    if (s->ev_planes[i]) (void)hipEventDestroy(s->ev_planes[i]);
+    if (s->fstream[i]) (void)hipStreamDestroy(s->fstream[i]);
+  }
 
   if (s->ev_eps) (void)hipEventDestroy(s->ev_eps);
   for (int i = 0; i < 3; ++i)
@@ -3622,7 +3647,7 @@ int pft_ipc_staged_env(void)
   return e && atoi(e) == 1;
 }
 
-int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, long fs, int device,
+int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, long fs, int remote,
                           int peer_staged)
 {
   if (side < 0 || side > 1) return -2;
@@ -3643,10 +3668,6 @@ int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, lo
     p.on = 1;
     return 0;
   }
-  // `device`: the peer GPU's pft_hip_device_phys_id, compared with ours
-  int mine = 0, dev = 0;
-  HIPCHK(hipGetDevice(&dev));
-  if (pft_hip_device_phys_id(dev, &mine)) return -1;
   const hipIpcMemHandle_t* h = (const hipIpcMemHandle_t*)handles;
   for (int b = 0; b <= PFT_BUF_COUNT + 1; ++b) {
     void* ptr = nullptr;
@@ -3662,7 +3683,7 @@ int pft_slab_ipc_set_peer(pft_slab* s, int side, const void* handles, int n3, lo
   }
   p.n3 = n3;
   p.fs = fs;
-  p.remote = device != mine;
+  p.remote = remote ? 1 : 0;   // the caller compared the GPUs' identities (pft_hip_device_ident)
   // A neighbour on another GPU writes into our receive buffer (uncached) rather than our ghost
   // planes, and we copy it in after the flag wait: no L2 of ours can hold a stale line of what it
   // wrote.  Both sides take the same decision: remote is symmetric, and the
@@ -3688,6 +3709,14 @@ int pft_slab_ipc_close(pft_slab* s)
     HIPCHK(hipMemset(s->sig, 0, 2 * sizeof(unsigned long long)));
     HIPCHK(hipDeviceSynchronize());
     s->ipc_poisoned = 0;
+  }
+  if ((s->peer[0].on && s->peer[0].opened) || (s->peer[1].on && s->peer[1].opened)) {
+    // the copy-engine exchange's streams write into the mappings about to be closed: drained first
+    // (they wait only on compute-stream work, which the detach's pft_slab_sync has drained)
+    if (s->comm) (void)hipStreamSynchronize(s->comm);
+    if (s->side) (void)hipStreamSynchronize(s->side);
+    for (int i = 0; i < 2; ++i)
+      if (s->fstream[i]) (void)hipStreamSynchronize(s->fstream[i]);
   }
   for (int side = 0; side < 2; ++side) {
     SlabPeer& p = s->peer[side];
@@ -3782,25 +3811,55 @@ int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsign
   if (!s->seqtab) {
     HIPCHK(hipMalloc((void**)&s->seqtab, sizeof(unsigned long long) * PFT_SEQTAB));
     HIPCHK(hipHostMalloc((void**)&s->seqhost, 2 * sizeof(unsigned long long) * PFT_SEQTAB, hipHostMallocDefault));
+    for (int i = 0; i < 2; ++i) HIPCHK(hipEventCreateWithFlags(&s->ev_seq[i], hipEventDisableTiming));
     s->seq_base = ~0ULL;
     // test hook PFT_CE_SEQTAB=n (2..4096): a table of n numbers, refilled every n exchanges
     const char* et = getenv("PFT_CE_SEQTAB");
     s->seq_n = (et && atoi(et) >= 2 && atoi(et) <= PFT_SEQTAB) ? atoi(et) : PFT_SEQTAB;
+    // the flag behind an explicit completion of the plane copies (default 1: one flag stream per
+    // side; 2: one flag stream for both sides; 0: the flag copy right behind the planes on the same
+    // stream, relying on the in-order SDMA queue)
+    const char* ef = getenv("PFT_CE_FENCE");
+    s->ce_fence = ef && atoi(ef) >= 0 && atoi(ef) <= 2 ? atoi(ef) : 1;
+    if (s->ce_fence) {
+      int lo = 0, hi = 0;
+      HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      for (int i = 0; i < 2; ++i) {
+        if (i == 0 || s->ce_fence == 1) HIPCHK(hipStreamCreateWithPriority(&s->fstream[i], hipStreamNonBlocking, hi));
+        HIPCHK(hipEventCreateWithFlags(&s->ev_planes[i], hipEventDisableTiming));
+      }
+    }
   }
   const int NSEQ = s->seq_n;
   if (s->seq_base == ~0ULL || seq <= s->seq_base || seq > s->seq_base + NSEQ) {
     // the next block of sequence numbers, from the pinned half not used by the previous refill
-    // (that one's copy is PFT_SEQTAB exchanges old: complete)
     s->seq_base = (seq - 1) / NSEQ * NSEQ;
     s->seq_half ^= 1;
-    if (s->ce_streams != 1) {
+    // the flag copies read the device table: the refill (comm stream) waits for the last flag copy
+    // of every other stream that reads it
+    if (s->ce_fence) {
+      for (int i = 0; i < 2; ++i) {
+        hipStream_t f = s->fstream[s->ce_fence == 1 ? i : 0];
+        HIPCHK(hipEventRecord(s->ev_planes[i], f));
+        HIPCHK(hipStreamWaitEvent(s->comm, s->ev_planes[i], 0));
+      }
+    } else if (s->ce_streams != 1) {
       // the side stream's last flag copy reads the old table: the refill (comm stream) waits for it
       HIPCHK(hipEventRecord(s->ev_side, s->side));
       HIPCHK(hipStreamWaitEvent(s->comm, s->ev_side, 0));
     }
+    // this pinned half was last read by the refill copy two refills ago: the host rewrites it only
+    // once that copy has run (with a small table -- the PFT_CE_SEQTAB test hook -- the speculative
+    // pipeline can hold that many exchanges queued)
+    // (bounded like every host wait with ipc peers: a lost peer can hold that copy's stream)
+    {
+      const int wrc = slab_wait(s, s->ev_seq[s->seq_half], "pft_slab_halo_put_ce (seqtab refill)");
+      if (wrc) return wrc;
+    }
     unsigned long long* h = s->seqhost + (size_t)s->seq_half * PFT_SEQTAB;
     for (int i = 0; i < NSEQ; ++i) h[i] = s->seq_base + 1 + i;
     HIPCHK(hipMemcpyAsync(s->seqtab, h, sizeof(unsigned long long) * NSEQ, hipMemcpyHostToDevice, s->comm));
+    HIPCHK(hipEventRecord(s->ev_seq[s->seq_half], s->comm));
     if (s->ce_streams != 1) {
       // the side stream's flag copies read the new table: this exchange's (and so every later one's)
       // follow the refill.  (An event on every exchange instead held each side flag behind the comm
@@ -3846,8 +3905,28 @@ int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsign
     }
   }
   const unsigned long long* sv = s->seqtab + (seq - 1 - s->seq_base);
-  if (s->peer[0].on) HIPCHK(hipMemcpyAsync(s->peer[0].sig + 1, sv, 8, hipMemcpyDeviceToDeviceNoCU, cs[0]));
-  if (s->peer[1].on) HIPCHK(hipMemcpyAsync(s->peer[1].sig + 0, sv, 8, hipMemcpyDeviceToDeviceNoCU, cs[1]));
+  // The neighbour reads the planes once it sees the flag, so the flag must not land before them.
+  // ce_fence (default): the flag copy goes on a stream of its own behind an event recorded after
+  // the side's plane copies.  The runtime turns that event wait into a dependency on the copies'
+  // completion signal (hsa_amd_memory_async_copy, hsa_ext_amd.h: "the copy will start after every
+  // [dependent] signal has been observed with the value 0", and the completion signal is
+  // decremented "when the copy operation is finished"), so the flag copy starts only after the
+  // plane copies have finished -- an ordering the HSA interface states, where a flag copy right
+  // behind them on the same stream relies on the SDMA queue retiring its writes in order (not a
+  // documented property across xGMI; PFT_CE_FENCE=0 restores that form for A/B).  The receiver's
+  // side is the system-scope acquire load of the flag in halo_wait_kernel (hsa_ext_amd.h asks the
+  // receiving device for a system-scope acquire before it uses a copy's destination).
+  hipStream_t fs[2] = {cs[0], cs[1]};
+  if (s->ce_fence) {
+    for (int side = 0; side < 2; ++side) {
+      if (!s->peer[side].on) continue;
+      HIPCHK(hipEventRecord(s->ev_planes[side], cs[side]));
+      fs[side] = s->fstream[s->ce_fence == 1 ? side : 0];
+      HIPCHK(hipStreamWaitEvent(fs[side], s->ev_planes[side], 0));
+    }
+  }
+  if (s->peer[0].on) HIPCHK(hipMemcpyAsync(s->peer[0].sig + 1, sv, 8, hipMemcpyDeviceToDeviceNoCU, fs[0]));
+  if (s->peer[1].on) HIPCHK(hipMemcpyAsync(s->peer[1].sig + 0, sv, 8, hipMemcpyDeviceToDeviceNoCU, fs[1]));
   return 0;
 }
 
@@ -3933,6 +4012,9 @@ int pft_slab_halo_wait(pft_slab* s, unsigned long long seq)
     if (s->peer[side].staged) sides |= 1 << side;
   }
   if (!w.f0 && !w.f1) return 0;
+  int local_staged = 0;
+  for (int side = 0; side < 2; ++side)
+    if (((sides >> side) & 1) && !s->peer[side].remote) local_staged = 1;
   int blocks = 1;
   if (sides) {
     // staged: what the neighbours put into the receive buffer, into the ghost planes of the
@@ -3948,18 +4030,7 @@ int pft_slab_halo_wait(pft_slab* s, unsigned long long seq)
     r.depth = s->put_deep ? 2 : 1;
     r.sides = sides;
     w.recv = 1;
-    const long n = 4L * r.nf * s->plane;
-    blocks = (int)std::min<long>(1024, std::max<long>(1, (n + 255) / 256));
-    // every block spins until the flags arrive: with a staged neighbour on this same GPU (the test
-    // hook PFT_IPC_STAGED between processes) a thousand spinning blocks leave no CU free for a
-    // pair kernel's workgroup (the whole register file) of the neighbour whose boundary raises the
-    // flag -- it would wait out PFT_IPC_TIMEOUT.  A few blocks then, which copy more each.
-    for (int side = 0; side < 2; ++side)
-      if (((sides >> side) & 1) && !s->peer[side].remote) blocks = std::min(blocks, 32);
-    // in the boundary pipeline the wait runs beside an interior launch and the next one does not
-    // wait for it: its blocks must not hold the CUs that launch's workgroups need (128 blocks of 4
-    // waves: 16 CUs' worth; the 20 MB of the receive still take ~10 us)
-    if (ws == s->bnd) blocks = std::min(blocks, 128);
+    blocks = pft_halo_wait_blocks(4L * r.nf * s->plane, local_staged, s->gpu_ranks, ws == s->bnd);
   }
   if (s->wait_streamops) {
     // A/B (PFT_WAIT_STREAMOPS=1): the runtime's stream waits, then a separate receive launch
@@ -3970,6 +4041,32 @@ int pft_slab_halo_wait(pft_slab* s, unsigned long long seq)
     halo_wait_kernel<<<blocks, 256, 0, ws>>>(w);
   }
   HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// Workgroups of one halo_wait_kernel launch with a staged receive of n doubles.  Every block spins
+// on the flags before it copies, so the count bounds the CUs a wait can hold while the neighbour
+// whose launch raises the flag may need them:
+//  - a staged neighbour on this same GPU (PFT_IPC_STAGED between processes), or any other rank
+//    sharing this GPU (gpu_ranks > 1: N ranks per GPU, whose neighbours may sit on another GPU and
+//    depend on a rank of ours): 32 blocks.  A thousand spinning blocks would leave no CU for a pair
+//    kernel's workgroup (the whole register file of a CU) of the rank that raises the flag, which
+//    then waits out PFT_IPC_TIMEOUT -- or, across two GPUs, closes a wait cycle through both;
+//  - in the boundary pipeline (the wait beside an interior launch that does not wait for it): 128
+//    blocks of 4 waves, 16 CUs' worth; the 20 MB of the receive still take ~10 us;
+//  - otherwise (this rank alone on its GPU, waiting on the compute stream): up to 1024.
+int pft_halo_wait_blocks(long n, int local_staged, int gpu_ranks, int on_boundary_stream)
+{
+  int blocks = (int)std::min<long>(1024, std::max<long>(1, (n + 255) / 256));
+  if (local_staged || gpu_ranks > 1) blocks = std::min(blocks, 32);
+  if (on_boundary_stream) blocks = std::min(blocks, 128);
+  return blocks;
+}
+
+int pft_slab_set_gpu_ranks(pft_slab* s, int n)
+{
+  if (!s || n < 1) return -2;
+  s->gpu_ranks = n;
   return 0;
 }
 

@@ -747,13 +747,29 @@ int pft_solver_ic_formulas_device(int nprog, const int * qs, const int * lens, c
 	if(nprog < 1 || !qs || !lens || !ops || !args || pft_model_get_grid(&g)) return -2;
 	pr = (pft_ic_prog*)calloc(nprog, sizeof(pft_ic_prog));
 	if(!pr) return -1;
-	/* compile every program first: the decision (device or host) is the same on every rank (the
-	   programs are), and the device is not touched unless all of them compile */
+	/* compile every program first: the device is not touched unless all of them compile.  The
+	   outcome is agreed across ranks before anything collective: 1 (stays on the host) and -2 (bad
+	   program) are the same on every rank, but -1 (out of memory in the compiler's tables) is local,
+	   and a rank returning early would leave the others in ensure_slab's attach rounds or the
+	   allreduce of ic_device_finish until the transport's timeout.  Every rank returns the same code:
+	   -1 over -2 over 1. */
 	for(p = 0; p < nprog && ok; p++) {
 		if(qs[p] < 0 || qs[p] > 2 || lens[p] < 1) { ok = 0; rc = -2; break; }
 		rc = pft_ic_compile(&g, lens[p], ops + off, args + off, &pr[p]);
 		off += lens[p];
 		if(rc) ok = 0;
+	}
+	if(pft_comm_size(comm()) > 1) {
+		long long v = rc == -1 ? 3 : (rc == -2 ? 2 : (rc == 1 ? 1 : (rc ? 3 : 0)));
+		int crc = pft_comm_allreduce_max_i64(comm(), &v);
+		if(crc) {
+			for(p = 0; p < nprog; p++) pft_ic_prog_free(&pr[p]);
+			free(pr);
+			R.last_status = crc;
+			return PFT_SOLVE_DEVICE_ERROR;
+		}
+		rc = v == 3 ? -1 : (v == 2 ? -2 : (v == 1 ? 1 : 0));
+		ok = rc == 0;
 	}
 	if(!ok) {
 		for(p = 0; p < nprog; p++) pft_ic_prog_free(&pr[p]);

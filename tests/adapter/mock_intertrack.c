@@ -10,6 +10,7 @@
  * RK_MPI_SA_cleanup (:2725), FreePrecalcData.  Then it writes the interior of u, p, gl.
  *
  *   mock_intertrack <params.txt> n1 n2 total_n3 L1 L2 L3 calc_mode tau tau_min delta final_time <out>
+ * (under mpirun with several ranks each rank writes its own slab to <out>.<rank>)
  * params.txt: the 30 model parameters (model.c:44-59 order), one per line (C99 hex floats ok).
  * data/spheres_positions.txt must exist in the working directory (equation.c:35).
  */
@@ -93,7 +94,14 @@ int main(int argc, char ** argv)
 		if((rc = RK_MPI_SA_init(3 * (int)S, MPI_COMM_WORLD, MPImaster))) { fprintf(stderr, "init %d\n", rc); MPI_Abort(MPI_COMM_WORLD, 7); }
 		if((rc = RK_MPI_SA_check_mem(&mem_dist))) { fprintf(stderr, "check_mem %d\n", rc); MPI_Abort(MPI_COMM_WORLD, 8); }
 		rc = RK_MPI_SA_solve(final_time, &eqSystem);
-		f = fopen(argv[13], "wb");
+		if(MPIprocs > 1) {
+			/* every rank writes its own slab: <out>.<rank> */
+			char name[4096];
+			snprintf(name, sizeof(name), "%s.%d", argv[13], MPIrank);
+			f = fopen(name, "wb");
+		} else {
+			f = fopen(argv[13], "wb");
+		}
 		fprintf(f, "%a %a %ld %ld %d\n", eqSystem.t, eqSystem.h, eqSystem.steps, eqSystem.steps_total, rc);
 		for(q = 0; q < 3; q++)
 			for(k = 0; k < n3; k++)

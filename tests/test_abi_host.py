@@ -180,3 +180,22 @@ def test_device_ic_rejects_conflicting_inputs(kw):
     formulas or an uninitialised solver is refused up front (ValueError, also under python -O)"""
     with pytest.raises(ValueError, match="device_ic"):
         P.Simulation(10, 10, 20, (1e-3, 1e-3, 2e-3), 0, np.zeros(len(P.PARAM_NAMES)), device_ic=True, **kw)
+
+
+@pytest.mark.parametrize("n,local_staged,gpu_ranks,bnd,want", [
+    (4 * 2 * 160000, 0, 1, 0, 1024),    # alone on its GPU, remote neighbours, compute stream: up to 1024
+    (4 * 2 * 160000, 0, 1, 1, 128),     # the boundary pipeline: beside an interior launch
+    (4 * 2 * 160000, 1, 2, 0, 32),      # a staged neighbour on this GPU (PFT_IPC_STAGED)
+    (4 * 2 * 160000, 0, 2, 0, 32),      # N ranks per GPU, remote neighbours: bounded all the same
+    (4 * 2 * 160000, 0, 4, 1, 32),
+    (1000, 0, 1, 0, 4),                 # small receives: one block per 256 doubles
+    (1, 1, 3, 1, 1),
+])
+def test_halo_wait_blocks_bound_every_layout(n, local_staged, gpu_ranks, bnd, want):
+    """pft_halo_wait_blocks: the spinning workgroups of a staged receive's wait, bounded so that they
+    never hold the CUs a neighbour's pair workgroup needs -- 32 whenever the GPU is shared by ranks
+    (any layout: a staged neighbour on it, or N ranks per GPU with neighbours elsewhere), 128 beside
+    an interior launch"""
+    L = P.lib()
+    L.pft_halo_wait_blocks.argtypes = [C.c_long, C.c_int, C.c_int, C.c_int]
+    assert L.pft_halo_wait_blocks(n, local_staged, gpu_ranks, bnd) == want

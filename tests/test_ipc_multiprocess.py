@@ -227,15 +227,21 @@ _BESIDE_ALL = {"PFT_CE_BND": "1"}
                                                               (3, 2, 1, (0, 2), _BESIDE_ALL),
                                                               (3, 2, 0, (0, 1, 2), _PIPE), (3, 2, 1, (0, 1, 2), _PIPE),
                                                               (3, 0, 1, (0, 1, 2), _PIPE), (3, 2, 1, (1,), _PIPE),
-                                                              (2, 2, 0, (0, 1), dict(_PIPE, PFT_CE_SEQTAB="3"))])
+                                                              (2, 2, 0, (0, 1), dict(_PIPE, PFT_CE_SEQTAB="3")),
+                                                              (3, 2, 1, (0, 1, 2), {"PFT_CE_FENCE": "0"}),
+                                                              (3, 2, 0, (0, 1, 2), {"PFT_CE_FENCE": "2"}),
+                                                              (3, 2, 1, (0, 1, 2), {"PFT_CE_FENCE": "2", "PFT_CE_SEQTAB": "3"})])
 def test_g20_processes_copy_engine_equal_reference(tmp_path, nranks, pair, staged, ce_ranks, xenv):
     """the boundary planes first, their exchange as SDMA copies and 8-byte flag copies on the comm
     stream beside the interior launch, the receiver's flag wait before the next launch: golden g20
     bit for bit with the pair kernels (two-plane halo) and one launch per stage, direct and staged.
     ce_ranks (1,): only the middle rank puts on the copy engines, its neighbours with the put
     kernel -- the receiving side is the same for both.  PFT_CE_SEQTAB 5: the flags' table of
-    sequence numbers refilled every 5 exchanges, hundreds of times over the run.  _SERIAL,
-    _BESIDE_ALL: the boundary launches' placement"""
+    sequence numbers refilled every 5 exchanges, hundreds of times over the run (each refill
+    waits for the copy that last read its pinned half).  _SERIAL, _BESIDE_ALL: the boundary
+    launches' placement.  PFT_CE_FENCE: the flag behind the plane copies' completion on a flag
+    stream per side (1, the default), one flag stream for both sides (2), or right behind them on
+    the copy stream (0)"""
     meta, A = O.load_case("g20")
     times = meta["traj_times"][:2]
     env = {r: dict({"PFT_IPC_CE": "1"} if r in ce_ranks else {}, **({"PFT_IPC_STAGED": "1"} if staged else {}),
@@ -363,3 +369,23 @@ def test_device_phys_id_names_the_gpu():
         assert a.value == b.value and a.value >= 0
         ids.append(a.value)
     assert len(set(ids)) == len(ids)
+
+
+@pytest.mark.gpu
+def test_device_ident_names_the_gpu():
+    """pft_hip_device_ident: PCI bus id with the function, then the UUID; stable, distinct per
+    visible GPU.  The ipc attach counts a neighbour as on this GPU only when the identities are
+    equal (partitions of one package differ in the function or the UUID)."""
+    import ctypes as C
+    import re
+    import torch
+    L = P.lib()
+    ids = []
+    for d in range(torch.cuda.device_count()):
+        a, b = C.create_string_buffer(80), C.create_string_buffer(80)
+        assert L.pft_hip_device_ident(d, a, 80) == 0 and L.pft_hip_device_ident(d, b, 80) == 0
+        assert a.value == b.value
+        assert re.fullmatch(rb"[0-9a-fA-F]{4}:[0-9a-fA-F]{2}:[0-9a-fA-F]{2}\.[0-9a-fA-F]/[0-9a-f]{32}", a.value), a.value
+        ids.append(a.value)
+    assert len(set(ids)) == len(ids)
+    assert L.pft_hip_device_ident(0, C.create_string_buffer(16), 16) == -2     # too small a buffer
