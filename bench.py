@@ -409,7 +409,8 @@ def main():
                    "gl_store_skipped": gl_keep, "pair_kernels": pairs,
                    "gated_steps": gated_steps, "gate_misses": gate_misses,
                    "tiles": ({str(k): ("cache" if v[0] == 0 else f"{2 * v[1]}x{v[2]} cells")
-                              for k, v in geo.items()} if geo else None)},
+                              for k, v in geo.items()} if geo else None),
+                   "pair_tile": pair_tile_text(L, n1, n2) if pairs else None},
         "roofline": roof,
         # whole step at its algorithmic bytes (21 doubles per cell-step with the pair kernels, 39
         # with one launch per stage), per GPU
@@ -832,6 +833,17 @@ def workload(grid_nodes, world, shape="cube", literal_cube=False, mode=0, domain
     base = PR.default_params(grid_nodes=grid_nodes, calc_mode=mode, L=Lc)
     return (grid_nodes, base, (base["n1"], base["n2"], base["n3"] * world),
             (base["L1"], base["L2"], base["L3"] * world))
+
+
+def pair_tile_text(L, n1, n2):
+    """the pair kernels' tile on this slab (pft_slab_pair_geometry) and the tiles per plane"""
+    tx, ty = C.c_int(), C.c_int()
+    L.pft_solver_slab.restype = C.c_void_p
+    L.pft_slab_pair_geometry.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    if L.pft_slab_pair_geometry(L.pft_solver_slab(), C.byref(tx), C.byref(ty)):
+        return None
+    nt = ((n1 + tx.value - 1) // tx.value) * ((n2 + ty.value - 1) // ty.value)
+    return f"{tx.value}x{ty.value} cells, {nt} tiles per plane"
 
 
 def kernel_name(stage, a, rc_path, n1, pairs=False, glx=False):

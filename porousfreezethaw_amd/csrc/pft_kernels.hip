@@ -1066,20 +1066,28 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
 // acting pair's own thread does -- so the mirrored stage-B input is the reference's bit for bit.
 // z neighbours of both levels are read from the plane rings (own pair: written by the thread
 // itself; x/y neighbours: written one iteration earlier, behind the barrier).
+//
+// Positions beyond the 512 threads (round 6, the 40 x 20 tile: 22 x 24 = 528 positions).  The
+// last ring row (py = ty + 3) is only read, as the y neighbours of stage A's last row; its
+// positions past thread 511 (at most PFT_PAIR_NEX, all in that row) are loaded by lanes 0..15 of
+// the last wave as LDS DMA (global_load_lds_dwordx4: no registers -- the kernel has none to spare
+// at 256 VGPRs) into the staging array lX one plane ahead, and at the next iteration's start the
+// same lanes combine them into stage A's input and store it into lA with the other positions'.
+// The taller tile evaluates stage B on 400 positions instead of 380 with the same wave-phases per
+// plane, n2 = 200 / 400 is cut into 10 / 20 tile rows with no idle row (19-row tiles: 11 / 22, the
+// last one half empty), and 400^3 runs its 50 tiles x 5 z-chunks in one round of 250 workgroups
+// (55 x 9 in two rounds before): DESIGN.md section 8.0.
 #define PFT_PBLOCK 512
-// LDS layout of a field plane: the even cells of the positions (first cell of each pair) in one
-// half, the odd cells PFT_PAIR_H doubles later, position (px, py) at slot PFT_PAIR_PADP + py LWP + px
-// of each half.  A wave's lanes hold consecutive positions, so every 8-byte LDS access (a cell, or
-// a neighbour one slot or one row away) is consecutive across lanes: no bank conflicts (64 banks of
-// 4 B; interleaved pairs read at a 16-byte lane stride were 2-way conflicts, SQ_LDS_BANK_CONFLICT
-// 0.44 of the LDS cycles of pair 4+5: profiles/r04a_pmc_pair_table.txt).  PFT_PAIR_H is a multiple
-// of 32 pairs, so a mirrored lane's access to the other half falls on its own banks.
+#define PFT_PAIR_NEX 16
+// LDS layout of a field plane: the positions' cell pairs side by side (16 bytes a slot, PairLds
+// below), position (px, py) at slot PFT_PAIR_PADP + py LWP + px.  (The layout with the even and
+// odd cells in two halves, conflict-free 8-byte accesses, was removed in round 5: PairLds.)
 #define PFT_PAIR_PADP 2         // slots before / after the positions of each half: the discarded
                                 // outer cell of a ring pair reads one slot beyond its row
-#define PFT_PAIR_H 512          // doubles per half (even / odd cells) of a field plane
-#define PFT_PAIR_HB 468         // slots of a stage-B plane in the interleaved layout (rows 1..ty+2)
+#define PFT_PAIR_H 532          // pair slots of a stage-A field plane (rows 0..ty+3 at the row pitch)
+#define PFT_PAIR_HB 488         // slots of a stage-B plane in the interleaved layout (rows 1..ty+2)
 // The row pitch LWP (pairs) is a template parameter, a compile-time constant so that every LDS
-// access is a per-lane base + an immediate offset: 22 (tiles up to 40 cells wide, 19 rows) or 12
+// access is a per-lane base + an immediate offset: 22 (tiles up to 40 cells wide, 20 rows) or 12
 // (up to 20 cells wide, 38 rows: n1 = 100 in 5 tiles of 20 where 40-wide tiles leave a sixth idle)
 // measured crossover (profiles/r05_pair_threshold.txt, stage launches against pair kernels forced):
 // 128^3 (2048 cells per CU) -10%, 136^3 (2456) -1.4%, 144^3 (2916) +16%, 152^3 (3429) +18%, 160^3
@@ -1223,12 +1231,36 @@ __device__ __forceinline__ dbl2 pair_in_B(const PairArgs& a, int q, const PairRa
 // halves (every access conflict-free, no 16-byte accesses, more address registers): pair 2+3
 // 0.357-0.359 ms against 0.352-0.356, pair 4+5 0.416-0.424 against 0.409-0.411 (a spill); the y
 // neighbours as two 8-byte reads: pair 2+3 0.362-0.365, pair 4+5 0.410-0.415.
-#define PFT_PAIR_OPN 384      // stage-B positions of a tile ((tx/2) ty, at most 380: pair_geometry_ok)
+#define PFT_PAIR_OPN 400      // stage-B positions of a tile ((tx/2) ty, at most 400: pair_geometry_ok)
 struct PairLds {
   __device__ static __forceinline__ dbl2 ld(const double* L, int p) { return ld2(L + 2 * p); }
   __device__ static __forceinline__ void st(double* L, int p, dbl2 v) { st2(L + 2 * p, v); }
   __device__ static __forceinline__ double cell(const double* L, int p, int s) { return L[2 * p + s]; }
 };
+
+// One 16-byte LDS DMA per active lane (global_load_lds_dwordx4): lane l of the wave writes the 16
+// bytes at g into LDS byte address lds + 16 l.  Inline asm rather than
+// __builtin_amdgcn_global_load_lds: hipcc treats the builtin's pending LDS write as a reason to wait
+// for vmcnt(0) at the next barrier and at the next use of an ordinary load -- it would drain the
+// look-ahead loads and the output stores every plane (MI355X guide, "Pipelining across barriers").
+// Invisible to the compiler, the DMA is ordered by hand: its reader waits with a counted vmcnt
+// (pair_x_wait), and the "memory" clobber keeps the reads of the previous plane's staging before it
+// and the look-ahead loads after it.  M0 is not used by any other instruction of these kernels.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void lds_dma16(unsigned lds, const void* base, unsigned off)
+{
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds), "v"(off), "s"(base) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+// the staging of the previous plane's DMA has landed: every vector-memory operation but the N
+// youngest is done (loads, stores and LDS DMA count together in issue order, MI355X guide), and at
+// least N loads -- that plane's look-ahead -- were issued after the DMA
+template <int N>
+__device__ __forceinline__ void pair_x_wait()
+{
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 // the RHS of one cell pair (du, dp of both cells): centre zc, z neighbours zm / zp, x/y
 // neighbours from the LDS field planes L[q] around slot p (even / odd halves, row pitch LWP); the
@@ -1310,7 +1342,13 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   // (without OPL a 1 x 1 placeholder: its accesses below sit in a branch that is constant-false
   // there, which -Warray-bounds flags per instantiation; an if constexpr would drop the placeholder
   // and shift the LDS layout of every other kernel)
-  __shared__ __attribute__((aligned(16))) dbl2 lO[OPL ? 6 : 1][OPL ? PFT_PAIR_OPN : 1];
+  // lO, then the extra positions' operands of the next plane (x u, p, gl; K1 u, p; K3 u, p), staged
+  // by LDS DMA (lX), in one array: the DMA's wave-uniform base lX - 16 (first loader lane) bytes
+  // must not fall below the LDS (without OPL a 20-slot pad takes lO's place)
+  constexpr int LXOFF = OPL ? 6 * PFT_PAIR_OPN : 20;
+  __shared__ __attribute__((aligned(16))) dbl2 lOX[LXOFF + 7 * PFT_PAIR_NEX];
+  dbl2(*const lO)[PFT_PAIR_OPN] = reinterpret_cast<dbl2(*)[PFT_PAIR_OPN]>(lOX);
+  dbl2* const lX = lOX + LXOFF;
 
   const int TX = a.tx, TY = a.ty, WP2 = TX / 2 + 2, NPOS = WP2 * (TY + 4);
   const int lin = xcd_remap(blockIdx.x, a.ntile * a.nchunk);
@@ -1341,6 +1379,56 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   const bool isB = (int)threadIdx.x < NPOS && px >= 1 && px <= TX / 2 && py >= 2 && py <= TY + 1 &&
                    pi < a.n1 && pj < a.n2;
   const int ob = (py - 2) * (TX / 2) + px - 1;                // this stage-B position's slot in lO
+  // positions beyond the threads (NPOS > PFT_PBLOCK: pair_geometry_ok puts them all in the last
+  // ring row ty + 3, columns px >= PFT_PBLOCK - WP2 (ty + 3)): the thread two rows below each (row
+  // ty + 1, same column -- threads PFT_PBLOCK - 2 WP2 .. (ty + 2) WP2 - 1, lanes 64 - 2 WP2 .. of
+  // the last wave) loads it too, by LDS DMA into lX one plane ahead like its own look-ahead, and
+  // stores its stage-A input into lA with its own.  Its acting pair is two rows above the loader's
+  // (clamped at the wall: a mirrored row's acting row is n2 - 1), its lA slot two rows above the
+  // loader's.  Everything about it is recomputed where used from the thread index, the acting
+  // offset apo and the phase's kernel arguments: the kernel holds no register for it across the
+  // loop (pair 4+5 is at 256 VGPRs).
+  auto xlo = [&](const PairArgs& A) { return PFT_PBLOCK - 2 * (A.tx / 2 + 2); };   // first loader thread
+  auto is_x = [&](const PairArgs& A) {
+    const int wp2 = A.tx / 2 + 2;
+    return wp2 * (A.ty + 4) > PFT_PBLOCK && (int)threadIdx.x >= xlo(A) && (int)threadIdx.x < wp2 * (A.ty + 2);
+  };
+  auto apo_x = [&](const PairArgs& A) {
+    const unsigned ajx = apo / (unsigned)A.n1;               // the loader's acting row
+    return apo + (unsigned)min(2, A.n2 - 1 - (int)ajx) * (unsigned)A.n1;
+  };
+  constexpr int NLA = SA == 4 ? 7 : 5;                        // loads of a position's operands (pair_load)
+  auto pboe = [&](const PairArgs& A, int m) -> unsigned { return ((unsigned)(m + 2) * (unsigned)A.plane + apo_x(A)) * 8u; };
+  // the DMA of plane m's operands of the extra position into lX (this lane: slot xs of each array)
+  auto dma = [&](const PairArgs& A, int m) {
+    const unsigned bo = pboe(A, m);
+    const unsigned l0 = (unsigned)(size_t)((__attribute__((address_space(3))) dbl2*)lX) -
+                        16u * (unsigned)(64 - 2 * (A.tx / 2 + 2));     // lane (64 - 2 WP2) -> slot 0
+    const unsigned fb = (unsigned)A.fs * 8u;                  // a field's bytes (pft_slab_pair_ok: 3 fb < 4 GiB)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) lds_dma16(l0 + (0 + q) * 16 * PFT_PAIR_NEX, A.x, bo + q * fb);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) lds_dma16(l0 + (3 + q) * 16 * PFT_PAIR_NEX, A.k1, bo + q * fb);
+    if (SA == 4) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) lds_dma16(l0 + (5 + q) * 16 * PFT_PAIR_NEX, A.k3, bo + q * fb);
+    }
+  };
+  // stage A's input of the extra position from the staging (after pair_x_wait), field by field,
+  // into the ring slot `slot` (its lA position: two rows above this thread's)
+  auto xstore = [&](const PairArgs& A, int slot) {
+    const int xs = (int)threadIdx.x - xlo(A);                 // this loader's slot in lX (0 .. 15)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      PairRaw t;
+      t.x[q] = lX[(0 + q) * PFT_PAIR_NEX + xs];
+      if (q < 2) {
+        t.k1[q] = lX[(3 + q) * PFT_PAIR_NEX + xs];
+        if (SA == 4) t.k3[q] = lX[(5 + q) * PFT_PAIR_NEX + xs];
+      }
+      LD::st(lA[slot][q], posA + 2 * LWP, pair_in_A<SA, GLX>(A, q, t));
+    }
+  };
 
   const int kb = a.k_begin + chunk * a.kz;
   const int ke = min(kb + a.kspan, a.k_end);
@@ -1404,6 +1492,24 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) fzA[s] = face_of(c, iam[1][s], iam[2][s], iam[0][s], ia0[1][s], ia0[2][s], ia0[0][s], FLUX);
+    if (is_x(a)) {
+      // the extra position: planes mA0 - 1 and mA0 as the others' (loaded here), mA0 + 1 by DMA,
+      // ahead of the look-ahead below (asm "memory" clobbers)
+      PairRaw t;
+      if (mA0 > mfirst) {
+        pair_load<SA>(a, pboe(a, mA0 - 1), t);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) LD::st(lA[2][q], posA + 2 * LWP, pair_in_A<SA, GLX>(a, q, t));
+      }
+      pair_load<SA>(a, pboe(a, mA0), t);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const dbl2 v = pair_in_A<SA, GLX>(a, q, t);
+        LD::st(lA[0][q], posA + 2 * LWP, v);
+        if (mA0 == mfirst) LD::st(lA[2][q], posA + 2 * LWP, v);
+      }
+      if (mA0 + 1 <= mlast && mA0 < ke) dma(a, mA0 + 1);
+    }
     if (mA0 + 1 <= mlast) pair_load<SA>(a, pbo(mA0 + 1), R[1]);
     KA[2][0] = KA[2][1] = zero2;
     __syncthreads();
@@ -1430,6 +1536,19 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
           LD::st(lA[sAp][q], posA, v);
           if (ZREG) IA[sAp][q] = v;
         }
+      }
+      if (is_x(A0)) {
+        // the extra position as this thread's own: plane mm + 1's operands from the staging (its
+        // DMA went out one iteration ago, ahead of that iteration's NLA look-ahead loads: all but
+        // the NLA - 1 youngest vector-memory operations done means it has landed), then plane
+        // mm + 2's DMA ahead of this iteration's look-ahead, after the staging's reads (asm
+        // "memory" clobbers) -- not in the chunk's last step, so that no DMA is left outstanding
+        // when the workgroup ends
+        if (mm + 1 <= mlast) {
+          pair_x_wait<NLA - 1>();
+          xstore(A0, sAp);
+        }
+        if (mm + 2 <= mlast && mm < ke) dma(A0, mm + 2);
       }
       if (mm + 2 <= mlast) pair_load<SA>(A0, pbo(mm + 2), rnn);          // look-ahead
     }
@@ -1993,11 +2112,10 @@ struct pft_slab {
   int seq_half, seq_n;
   hipEvent_t ev_seq[2];  // recorded after each refill's H2D copy from that pinned half: the host
                          // rewrites a half only once the copy that read it last has run
-  // the flag behind the completed plane copies (pft_slab_halo_put_ce, ce_fence): per side an event
-  // after its plane copies and a flag stream that waits for it
+  // the flags behind the completed plane copies (pft_slab_halo_put_ce, ce_fence): an event after
+  // each copy stream's planes, waited for by the OTHER copy stream, which raises that side's flag
   int ce_fence;
   int gpu_ranks;         // ranks of the communicator on this slab's GPU (ipc attach; 0/1: alone)
-  hipStream_t fstream[2];
   hipEvent_t ev_planes[2];
   // boundary launches on their own stream (pft_slab_set_boundary_stream; the copy-engine exchange):
   // a launch of the boundary planes (PFT_K_BOUNDARY/2) runs on `bnd` beside the interior launch on
@@ -2386,7 +2504,6 @@ int pft_slab_destroy(pft_slab* s)
   for (int i = 0; i < 2; ++i) {
     if (s->ev_seq[i]) (void)hipEventDestroy(s->ev_seq[i]);
     if (s->ev_planes[i]) (void)hipEventDestroy(s->ev_planes[i]);
-    if (s->fstream[i]) (void)hipStreamDestroy(s->fstream[i]);
   }
 
   if (s->ev_eps) (void)hipEventDestroy(s->ev_eps);
@@ -3389,32 +3506,39 @@ static int pair_lwp(int tx) { return tx <= 20 ? 12 : 22; }
 static bool pair_geometry_ok(int tx, int ty)
 {
   const int lwp = pair_lwp(tx);
-  return tx >= 2 && tx % 2 == 0 && ty >= 1 && (tx / 2 + 2) * (ty + 4) <= PFT_PBLOCK && tx / 2 + 2 <= 22 &&
+  // positions: one per thread, and up to PFT_PAIR_NEX more in the last ring row (LDS DMA)
+  return tx >= 2 && tx % 2 == 0 && ty >= 1 && (tx / 2 + 2) * (ty + 4) <= PFT_PBLOCK + PFT_PAIR_NEX &&
+         (tx / 2 + 2) * (ty + 3) <= PFT_PBLOCK && tx / 2 + 2 <= 22 &&
          2 * PFT_PAIR_PADP + lwp * (ty + 4) <= PFT_PAIR_H && 2 * PFT_PAIR_PADP + lwp * (ty + 2) <= PFT_PAIR_HB &&
          (tx / 2) * ty <= PFT_PAIR_OPN;
 }
 
 // automatic tile: the fewest workgroups per plane (a workgroup-plane costs about the same whatever
 // the tile's edge tiles hold), of those the one with the fewest idle tile cells, then the wider.
-// n1 = 200 / 400: 40 x 19 cells (5 x 11 / 10 x 22 tiles, 462 of 512 threads evaluate stage A and
-// 380 stage B); n1 = 100: 20 x 34 cells (5 x 3 tiles, 98% of their cells in the plane, against 18
+// n1 = 200 / 400: 40 x 20 cells (5 x 10 / 10 x 20 tiles, 484 of 512 threads evaluate stage A and
+// 400 stage B, 16 positions of the last ring row DMA-staged; 40 x 19 before round 6); n1 = 100: 20 x 34 cells (5 x 3 tiles, 98% of their cells in the plane, against 18
 // 34 x 19 tiles with the 22-pair pitch alone).  Returns the tiles per plane, 0 when no tile fits
 // (n1 odd).
 static long pair_geometry(int n1, int n2, int* tx_out, int* ty_out)
 {
   long best = 0, best_idle = 0;
-  int bx = 0, by = 0;
+  int bx = 0, by = 0, bleg = 0;
   if (n1 < 2 || n1 % 2 || n2 < 1) return 0;
   for (int tx = 2; tx <= n1 + 1 && tx <= 40; tx += 2) {
     for (int ty = std::min(n2, PFT_PBLOCK); ty >= 1; --ty) {
       if (!pair_geometry_ok(tx, ty)) continue;
       const long nt = (long)((n1 + tx - 1) / tx) * ((n2 + ty - 1) / ty);
       const long idle = nt * tx * ty - (long)n1 * n2;
-      if (best == 0 || nt < best || (nt == best && idle <= best_idle)) {
+      // on a tie, a tile the round-5 limits allowed (one position per thread, 512 / 468 / 384 LDS
+      // slots) keeps its place: the measured choices there (n1 = 100: 20 x 34) stay as they were
+      const int leg = (tx / 2 + 2) * (ty + 4) <= PFT_PBLOCK && 2 * PFT_PAIR_PADP + pair_lwp(tx) * (ty + 4) <= 512 &&
+                      2 * PFT_PAIR_PADP + pair_lwp(tx) * (ty + 2) <= 468 && (tx / 2) * ty <= 384;
+      if (best == 0 || nt < best || (nt == best && (idle < best_idle || (idle == best_idle && leg >= bleg)))) {
         best = nt;
         best_idle = idle;
         bx = tx;
         by = ty;
+        bleg = leg;
       }
     }
   }
@@ -3584,9 +3708,10 @@ int pft_slab_pair_ok(const pft_slab* s)
   // plane would need the neighbour's u_noise there (not exchanged: one launch per stage then)
   const bool nb = s->d.has_below || s->d.has_above;
   if (nb && (s->d.n3 < 2 || s->noise)) return 0;
-  // (merson_pair addresses a field with 32-bit byte offsets)
+  // (merson_pair addresses a field with 32-bit byte offsets, and the extra positions' LDS DMA the
+  // three fields of a buffer from one base: 3 fields < 4 GiB, 178 M cells per slab)
   return s->pair_on && slab_kind(s) == KFUSED &&
-         (double)s->fs * 8.0 < 4294967296.0 && s->pair_ntile > 0;
+         3.0 * (double)s->fs * 8.0 < 4294967296.0 && s->pair_ntile > 0;
 }
 
 int pft_slab_pair_geometry(const pft_slab* s, int* tx, int* ty)
@@ -3715,8 +3840,6 @@ int pft_slab_ipc_close(pft_slab* s)
     // (they wait only on compute-stream work, which the detach's pft_slab_sync has drained)
     if (s->comm) (void)hipStreamSynchronize(s->comm);
     if (s->side) (void)hipStreamSynchronize(s->side);
-    for (int i = 0; i < 2; ++i)
-      if (s->fstream[i]) (void)hipStreamSynchronize(s->fstream[i]);
   }
   for (int side = 0; side < 2; ++side) {
     SlabPeer& p = s->peer[side];
@@ -3816,34 +3939,18 @@ int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsign
     // test hook PFT_CE_SEQTAB=n (2..4096): a table of n numbers, refilled every n exchanges
     const char* et = getenv("PFT_CE_SEQTAB");
     s->seq_n = (et && atoi(et) >= 2 && atoi(et) <= PFT_SEQTAB) ? atoi(et) : PFT_SEQTAB;
-    // the flag behind an explicit completion of the plane copies (default 1: one flag stream per
-    // side; 2: one flag stream for both sides; 0: the flag copy right behind the planes on the same
-    // stream, relying on the in-order SDMA queue)
+    // the flags behind an explicit completion of the plane copies (default 1; PFT_CE_FENCE=0: each
+    // flag copy right behind its planes on the same stream, relying on the in-order SDMA queue)
     const char* ef = getenv("PFT_CE_FENCE");
-    s->ce_fence = ef && atoi(ef) >= 0 && atoi(ef) <= 2 ? atoi(ef) : 1;
-    if (s->ce_fence) {
-      int lo = 0, hi = 0;
-      HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-      for (int i = 0; i < 2; ++i) {
-        if (i == 0 || s->ce_fence == 1) HIPCHK(hipStreamCreateWithPriority(&s->fstream[i], hipStreamNonBlocking, hi));
-        HIPCHK(hipEventCreateWithFlags(&s->ev_planes[i], hipEventDisableTiming));
-      }
-    }
+    s->ce_fence = !(ef && atoi(ef) == 0);
+    for (int i = 0; i < 2; ++i) HIPCHK(hipEventCreateWithFlags(&s->ev_planes[i], hipEventDisableTiming));
   }
   const int NSEQ = s->seq_n;
   if (s->seq_base == ~0ULL || seq <= s->seq_base || seq > s->seq_base + NSEQ) {
     // the next block of sequence numbers, from the pinned half not used by the previous refill
     s->seq_base = (seq - 1) / NSEQ * NSEQ;
     s->seq_half ^= 1;
-    // the flag copies read the device table: the refill (comm stream) waits for the last flag copy
-    // of every other stream that reads it
-    if (s->ce_fence) {
-      for (int i = 0; i < 2; ++i) {
-        hipStream_t f = s->fstream[s->ce_fence == 1 ? i : 0];
-        HIPCHK(hipEventRecord(s->ev_planes[i], f));
-        HIPCHK(hipStreamWaitEvent(s->comm, s->ev_planes[i], 0));
-      }
-    } else if (s->ce_streams != 1) {
+    if (s->ce_streams != 1) {
       // the side stream's last flag copy reads the old table: the refill (comm stream) waits for it
       HIPCHK(hipEventRecord(s->ev_side, s->side));
       HIPCHK(hipStreamWaitEvent(s->comm, s->ev_side, 0));
@@ -3916,14 +4023,22 @@ int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsign
   // documented property across xGMI; PFT_CE_FENCE=0 restores that form for A/B).  The receiver's
   // side is the system-scope acquire load of the flag in halo_wait_kernel (hsa_ext_amd.h asks the
   // receiving device for a system-scope acquire before it uses a copy's destination).
+  // No stream is added for it: a process has 4 hardware queues (GPU_MAX_HW_QUEUES) and already 4
+  // streams (compute, boundary, comm, side); a fifth and sixth share queues with them, and their
+  // waits then hold up unrelated work -- one flag stream per side measured that way (DESIGN
+  // section 6).  So each side's flag goes on the OTHER copy stream, behind an event after this
+  // side's planes: with two neighbours both flags land after both sides' planes (the two run side
+  // by side, of equal size), each ordered after its own planes by the event.  With one copy stream
+  // (ce_streams 1) the stream order is all there is.
   hipStream_t fs[2] = {cs[0], cs[1]};
-  if (s->ce_fence) {
-    for (int side = 0; side < 2; ++side) {
-      if (!s->peer[side].on) continue;
-      HIPCHK(hipEventRecord(s->ev_planes[side], cs[side]));
-      fs[side] = s->fstream[s->ce_fence == 1 ? side : 0];
-      HIPCHK(hipStreamWaitEvent(fs[side], s->ev_planes[side], 0));
-    }
+  if (s->ce_fence && cs[1] != cs[0]) {
+    for (int side = 0; side < 2; ++side)
+      if (s->peer[side].on) HIPCHK(hipEventRecord(s->ev_planes[side], cs[side]));
+    for (int side = 0; side < 2; ++side)
+      if (s->peer[side].on) {
+        fs[side] = cs[1 - side];
+        HIPCHK(hipStreamWaitEvent(fs[side], s->ev_planes[side], 0));
+      }
   }
   if (s->peer[0].on) HIPCHK(hipMemcpyAsync(s->peer[0].sig + 1, sv, 8, hipMemcpyDeviceToDeviceNoCU, fs[0]));
   if (s->peer[1].on) HIPCHK(hipMemcpyAsync(s->peer[1].sig + 0, sv, 8, hipMemcpyDeviceToDeviceNoCU, fs[1]));

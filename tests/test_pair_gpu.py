@@ -55,10 +55,36 @@ def _same(a, b):
     assert np.array_equal(a[4], b[4])
 
 
-# pair tiles (pair_geometry): 30 -> 30 cells wide (one tile), 100x36 -> 34 x 16 ish, 18x12 one
-# tile, 66x38 partial x tile, 252x14 / 318x10 wide planes, 2 x 6 and 4 x 130 narrow ones
+# pair tiles (pair_geometry): 30 -> 30 cells wide (one tile), 100x36 -> 20 x 36, 18x12 one
+# tile, 66x38 partial x tile, 252x14 / 318x10 wide planes, 2 x 6 and 4 x 130 narrow ones; the 40 x 20
+# tile of the 400^3 bench, whose last ring row holds 16 positions beyond the 512 threads (LDS DMA):
+# 80x40 (2 x 2 tiles, every one at two walls), 120x60 (3 x 3, an interior tile), 40x40 (one column)
 GRIDS = [(30, 30, 60), (100, 36, 40), (18, 12, 30), (66, 38, 21), (252, 14, 6), (318, 10, 5), (2, 6, 5),
-         (4, 130, 9), (50, 50, 100), (30, 30, 2)]
+         (4, 130, 9), (50, 50, 100), (30, 30, 2), (80, 40, 30), (120, 60, 20), (40, 40, 8)]
+TALL = [(80, 40, 30), (120, 60, 20), (40, 40, 8)]
+
+
+@pytest.mark.parametrize("dims", TALL)
+def test_tall_tile_geometry(dims):
+    """those grids do run the 40 x 20 tile (pft_slab_pair_geometry)"""
+    meta, _ = O.load_case("g20")
+    Pm, info = O.params_from_meta(meta)
+    n1, n2, n3 = dims
+    L = P.lib()
+    L.pft_solver_set_option(P.PFT_OPT_PAIR, 2)
+    try:
+        sim = P.Simulation(n1, n2, n3, (info["L1"], info["L2"], info["L3"]), 0, Pm, beads=O.beads(), tau=1.0,
+                           tau_min=info["tau_min"], delta=info["delta"], tile=2)
+        assert sim.solve_ex(1e9, 1, 0) == 2
+        tx, ty = C.c_int(), C.c_int()
+        L.pft_solver_slab.restype = C.c_void_p
+        L.pft_slab_pair_geometry.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        assert L.pft_slab_pair_geometry(L.pft_solver_slab(), C.byref(tx), C.byref(ty)) == 0
+        assert (tx.value, ty.value) == (40, 20)
+        assert sim.stats().pairs == 1
+        sim.close()
+    finally:
+        L.pft_solver_set_option(P.PFT_OPT_PAIR, 1)
 
 
 @pytest.mark.parametrize("dims", GRIDS)
@@ -72,7 +98,7 @@ def test_pair_equals_stage_kernels(dims, mode):
 
 
 @pytest.mark.parametrize("kz", [1, 2, 3, 7])
-@pytest.mark.parametrize("dims", [(30, 30, 60), (66, 38, 21), (2, 6, 5)])
+@pytest.mark.parametrize("dims", [(30, 30, 60), (66, 38, 21), (2, 6, 5), (80, 40, 30)])
 def test_pair_z_chunks(dims, kz):
     """forced z-chunks: every chunk but the first recomputes stage A on the plane below its first,
     every chunk but the last on the plane above its last (one plane per chunk at kz = 1)"""
@@ -94,7 +120,7 @@ def test_pair_gl_static_and_noise(gl_static, noise, mode):
 
 
 @pytest.mark.parametrize("kz", [None, 2])
-@pytest.mark.parametrize("dims", [(66, 38, 21), (30, 30, 60)])
+@pytest.mark.parametrize("dims", [(66, 38, 21), (30, 30, 60), (120, 60, 20)])
 def test_pair_gl_negative_zero(dims, kz):
     """a -0.0 in gl turns gl_keep off (pft_slab_set_gl_keep): the pair kernels without GLX, whose
     stage B keeps gl in its own ring and re-loads the operands of its outputs (no lO), against the
@@ -132,7 +158,7 @@ def test_pair_gl_negative_zero(dims, kz):
     assert np.array_equal(got[4], res[5]) and np.array_equal(np.signbit(got[4][2]), np.signbit(res[5][2]))
 
 
-@pytest.mark.parametrize("dims", [(30, 30, 60), (100, 36, 40), (18, 12, 30)])
+@pytest.mark.parametrize("dims", [(30, 30, 60), (100, 36, 40), (18, 12, 30), (80, 40, 30)])
 def test_pair_matches_oracle(dims):
     got, used, ic, info, Pm = _run(dims, 0, True, 12)
     n1, n2, n3 = dims
@@ -176,7 +202,7 @@ def test_pair_golden_trajectory(mode, gl_static):
 
 def test_pair_full_size_400():
     """BASELINE configs[1] (200 x 200 x 400, beads): 20 attempted steps with and without pairs, and
-    the pair tile the bench runs (40 x 19 cells)"""
+    the pair tile the bench runs (40 x 20 cells, 16 DMA-staged positions)"""
     got, used, *_ = _run((200, 200, 400), 0, True, 20, tile=1)
     ref, *_ = _run((200, 200, 400), 0, False, 20, tile=1)
     assert used == 1
@@ -240,7 +266,7 @@ def test_pair_multislab_loopback_golden(nprocs, gl_static):
         assert np.array_equal(np.concatenate([o[0][i][5] for o in out], axis=1), A[f"traj_m0_state{i}"])
 
 
-@pytest.mark.parametrize("nprocs,dims", [(3, (30, 30, 60)), (4, (66, 38, 21)), (2, (100, 36, 40)),
+@pytest.mark.parametrize("nprocs,dims", [(3, (30, 30, 60)), (4, (66, 38, 21)), (2, (100, 36, 40)), (3, (80, 40, 30)),
                                           (4, (30, 30, 12)), (3, (18, 12, 8))])
 def test_pair_multislab_loopback_equals_one_slab(nprocs, dims):
     """default IC on grids with partial tiles and uneven slabs (21 planes over 4: 6/5/5/5; slabs of
