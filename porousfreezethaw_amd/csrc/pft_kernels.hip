@@ -1254,8 +1254,7 @@ __device__ __forceinline__ void lds_dma16(unsigned lds, const void* base, unsign
 }
 #pragma clang diagnostic pop
 // the staging of the previous plane's DMA has landed: every vector-memory operation but the N
-// youngest is done (loads, stores and LDS DMA count together in issue order, MI355X guide), and at
-// least N loads -- that plane's look-ahead -- were issued after the DMA
+// youngest is done (loads, stores and LDS DMA count together in issue order, MI355X guide)
 template <int N>
 __device__ __forceinline__ void pair_x_wait()
 {
@@ -1308,6 +1307,36 @@ __device__ __forceinline__ void pair_rhs(const pft_consts& c, const double* L0, 
   }
 }
 
+// Thread (virtual position index v) -> position (px, py) of a tile of bw = tx/2 stage-B pairs x ty
+// rows (round 6), for tiles with positions beyond the threads: whole rows of the R2 tile, each
+// row contiguous (wp2 = bw + 2 pairs, so every load and store of a row is one run, as row-major),
+// but in the order: stage B's rows 2 .. ty + 1 first, then stage A's ring rows 1 and ty + 2, then
+// the load-only rows 0 and ty + 3 -- the last of them beyond the threads (pair_geometry_ok: at most
+// PFT_PAIR_NEX, all in row ty + 3).  With 22-pair rows (40 x 20 tile) stage B's 20 rows end at
+// thread 439, so the last wave (448 .. 511) holds ring rows only and skips stage B: its SIMD runs 3
+// wave-phases a plane where the others run 4, and the extra positions' staging and DMA ride in that
+// slack instead of delaying the barrier.  (Stage-B positions compacted to threads 0 .. 399, ring
+// columns after them, did the same for pair 2+3 but cost pair 4+5 9%: its rows no longer one run;
+// profiles/r06_ab_pair_tile.txt.)  Row-major from row 0 for tiles without extra positions.
+__device__ __forceinline__ void pair_pos(int v, int bw, int ty, int& px, int& py)
+{
+  const int wp2 = bw + 2;
+  if (v < ty * wp2) {                                  // stage B's rows
+    py = 2 + v / wp2;
+    px = v % wp2;
+    return;
+  }
+  v -= ty * wp2;
+  if (v < 2 * wp2) {                                   // stage A's ring rows
+    py = v < wp2 ? 1 : ty + 2;
+    px = v < wp2 ? v : v - wp2;
+    return;
+  }
+  v -= 2 * wp2;                                        // load-only rows
+  py = v < wp2 ? 0 : ty + 3;
+  px = v < wp2 ? v : v - wp2;
+}
+
 template <int N>
 using pft_ic = std::integral_constant<int, N>;
 
@@ -1344,11 +1373,14 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   // and shift the LDS layout of every other kernel)
   // lO, then the extra positions' operands of the next plane (x u, p, gl; K1 u, p; K3 u, p), staged
   // by LDS DMA (lX), in one array: the DMA's wave-uniform base lX - 16 (first loader lane) bytes
-  // must not fall below the LDS (without OPL a 20-slot pad takes lO's place)
-  constexpr int LXOFF = OPL ? 6 * PFT_PAIR_OPN : 20;
+  // must not fall below the LDS (without OPL a 64-slot pad takes lO's place)
+  constexpr int LXOFF = OPL ? 6 * PFT_PAIR_OPN : 64;
   __shared__ __attribute__((aligned(16))) dbl2 lOX[LXOFF + 7 * PFT_PAIR_NEX];
   dbl2(*const lO)[PFT_PAIR_OPN] = reinterpret_cast<dbl2(*)[PFT_PAIR_OPN]>(lOX);
   dbl2* const lX = lOX + LXOFF;
+  // the extra positions' acting-pair offsets, set once (the tile's corner x0, y0 is not kept live
+  // across the loop for them: pair 4+5 has no register or SGPR to spare)
+  __shared__ unsigned lXa[PFT_PAIR_NEX];
 
   const int TX = a.tx, TY = a.ty, WP2 = TX / 2 + 2, NPOS = WP2 * (TY + 4);
   const int lin = xcd_remap(blockIdx.x, a.ntile * a.nchunk);
@@ -1356,7 +1388,15 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   const int x0 = (tile % a.ntx) * TX, y0 = (tile / a.ntx) * TY;
   // threads beyond the R2 positions shadow the last one (same loads and LDS writes, no stores)
   const int tt = min((int)threadIdx.x, NPOS - 1);
-  const int px = tt % WP2, py = tt / WP2;
+  int px, py;
+  if (NPOS > PFT_PBLOCK) {
+    pair_pos(tt, TX / 2, TY, px, py);
+  } else {
+    // no extra positions: row-major over the R2 tile, as measured best there (200^3: the stage-B
+    // positions first ran 8% slower, profiles/r06_ab_pair_tile.txt)
+    px = tt % WP2;
+    py = tt / WP2;
+  }
   const int pi = x0 - 2 + 2 * px, pj = y0 - 2 + py;          // position: first cell, row
   // acting pair (in the domain): a mirrored position holds its values (x halves exchanged)
   const int ai = pi < 0 ? 0 : (pi >= a.n1 ? a.n1 - 2 : pi);
@@ -1380,30 +1420,33 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
                    pi < a.n1 && pj < a.n2;
   const int ob = (py - 2) * (TX / 2) + px - 1;                // this stage-B position's slot in lO
   // positions beyond the threads (NPOS > PFT_PBLOCK: pair_geometry_ok puts them all in the last
-  // ring row ty + 3, columns px >= PFT_PBLOCK - WP2 (ty + 3)): the thread two rows below each (row
-  // ty + 1, same column -- threads PFT_PBLOCK - 2 WP2 .. (ty + 2) WP2 - 1, lanes 64 - 2 WP2 .. of
-  // the last wave) loads it too, by LDS DMA into lX one plane ahead like its own look-ahead, and
-  // stores its stage-A input into lA with its own.  Its acting pair is two rows above the loader's
-  // (clamped at the wall: a mirrored row's acting row is n2 - 1), its lA slot two rows above the
-  // loader's.  Everything about it is recomputed where used from the thread index, the acting
-  // offset apo and the phase's kernel arguments: the kernel holds no register for it across the
-  // loop (pair 4+5 is at 256 VGPRs).
-  auto xlo = [&](const PairArgs& A) { return PFT_PBLOCK - 2 * (A.tx / 2 + 2); };   // first loader thread
-  auto is_x = [&](const PairArgs& A) {
-    const int wp2 = A.tx / 2 + 2;
-    return wp2 * (A.ty + 4) > PFT_PBLOCK && (int)threadIdx.x >= xlo(A) && (int)threadIdx.x < wp2 * (A.ty + 2);
+  // ring row ty + 3, the tail of pair_pos's order): the last NPOS - PFT_PBLOCK threads (lanes
+  // 64 - NEX .. 63 of the last wave, themselves load-only positions) load one each too, by LDS DMA
+  // into lX one plane ahead like their own look-ahead, and store its stage-A input into lA with
+  // their own.  Everything about it is recomputed where used from the thread index and the phase's
+  // kernel arguments (mostly scalar): the kernel holds no register for it across the loop (pair
+  // 4+5 is at 256 VGPRs).
+  auto nex = [&](const PairArgs& A) { return (A.tx / 2 + 2) * (A.ty + 4) - PFT_PBLOCK; };
+  // the loaders are lanes 64 - NEX .. 63 of the last wave; inside the z-loop they are found from
+  // the wave's index (one SGPR) and the lane index (mbcnt, recomputed): keeping threadIdx.x live
+  // across the loop for them cost pair 4+5 a spilled VGPR
+  const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  auto lane = [&]() {
+    int l;  // volatile: recomputed where used, so nothing derived from it is hoisted out of the loop
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
   };
-  auto apo_x = [&](const PairArgs& A) {
-    const unsigned ajx = apo / (unsigned)A.n1;               // the loader's acting row
-    return apo + (unsigned)min(2, A.n2 - 1 - (int)ajx) * (unsigned)A.n1;
-  };
-  constexpr int NLA = SA == 4 ? 7 : 5;                        // loads of a position's operands (pair_load)
+  auto is_x = [&](const PairArgs& A) { return wid == PFT_PBLOCK / 64 - 1 && lane() >= 64 - nex(A); };
+  // the extra position's column (row ty + 3) and its acting pair's offset in a plane
+  auto px_x = [&](const PairArgs& A) { return lane() - 64 + (A.tx / 2 + 2); };
+  auto apo_x = [&](const PairArgs& A) { return lXa[lane() - (64 - nex(A))]; };
+  auto pos_x = [&](const PairArgs& A) { return PFT_PAIR_PADP + (A.ty + 3) * LWP + px_x(A); };
   auto pboe = [&](const PairArgs& A, int m) -> unsigned { return ((unsigned)(m + 2) * (unsigned)A.plane + apo_x(A)) * 8u; };
   // the DMA of plane m's operands of the extra position into lX (this lane: slot xs of each array)
   auto dma = [&](const PairArgs& A, int m) {
     const unsigned bo = pboe(A, m);
     const unsigned l0 = (unsigned)(size_t)((__attribute__((address_space(3))) dbl2*)lX) -
-                        16u * (unsigned)(64 - 2 * (A.tx / 2 + 2));     // lane (64 - 2 WP2) -> slot 0
+                        16u * (unsigned)(64 - nex(A));       // lane 64 - NEX -> slot 0
     const unsigned fb = (unsigned)A.fs * 8u;                  // a field's bytes (pft_slab_pair_ok: 3 fb < 4 GiB)
 #pragma unroll
     for (int q = 0; q < 3; ++q) lds_dma16(l0 + (0 + q) * 16 * PFT_PAIR_NEX, A.x, bo + q * fb);
@@ -1415,9 +1458,10 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
     }
   };
   // stage A's input of the extra position from the staging (after pair_x_wait), field by field,
-  // into the ring slot `slot` (its lA position: two rows above this thread's)
+  // into the ring slot `slot`
   auto xstore = [&](const PairArgs& A, int slot) {
-    const int xs = (int)threadIdx.x - xlo(A);                 // this loader's slot in lX (0 .. 15)
+    const int xs = lane() - (64 - nex(A));                   // this loader's slot in lX (0 .. NEX - 1)
+    const int pe = pos_x(A);
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       PairRaw t;
@@ -1426,7 +1470,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
         t.k1[q] = lX[(3 + q) * PFT_PAIR_NEX + xs];
         if (SA == 4) t.k3[q] = lX[(5 + q) * PFT_PAIR_NEX + xs];
       }
-      LD::st(lA[slot][q], posA + 2 * LWP, pair_in_A<SA, GLX>(A, q, t));
+      LD::st(lA[slot][q], pe, pair_in_A<SA, GLX>(A, q, t));
     }
   };
 
@@ -1464,6 +1508,11 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   // prologue: stage A's input of planes mA0 - 1 (if any) and mA0 into the ring (slots 2 and 0);
   // operands of mA0 kept, of mA0 + 1 in flight.  (kb >= ke: an empty chunk, which still takes
   // part in the error norm's workgroup count below)
+  if (is_x(a)) {
+    const int ajx = min(y0 - 2 + a.ty + 3, a.n2 - 1);
+    const int aix = min(max(x0 - 2 + 2 * px_x(a), 0), a.n1 - 2);
+    lXa[(int)threadIdx.x - (PFT_PBLOCK - nex(a))] = (unsigned)(ajx * a.n1 + aix);
+  }
   if (kb < ke) {
     dbl2 ia0[3], iam[3];
     pair_load<SA>(a, pbo(mA0), R[0]);
@@ -1493,22 +1542,21 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
 #pragma unroll
     for (int s = 0; s < 2; ++s) fzA[s] = face_of(c, iam[1][s], iam[2][s], iam[0][s], ia0[1][s], ia0[2][s], ia0[0][s], FLUX);
     if (is_x(a)) {
-      // the extra position: planes mA0 - 1 and mA0 as the others' (loaded here), mA0 + 1 by DMA,
-      // ahead of the look-ahead below (asm "memory" clobbers)
+      // the extra position: planes mA0 - 1 and mA0 as the others' (loaded here), mA0 + 1 by DMA
       PairRaw t;
       if (mA0 > mfirst) {
         pair_load<SA>(a, pboe(a, mA0 - 1), t);
 #pragma unroll
-        for (int q = 0; q < 3; ++q) LD::st(lA[2][q], posA + 2 * LWP, pair_in_A<SA, GLX>(a, q, t));
+        for (int q = 0; q < 3; ++q) LD::st(lA[2][q], pos_x(a), pair_in_A<SA, GLX>(a, q, t));
       }
       pair_load<SA>(a, pboe(a, mA0), t);
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         const dbl2 v = pair_in_A<SA, GLX>(a, q, t);
-        LD::st(lA[0][q], posA + 2 * LWP, v);
-        if (mA0 == mfirst) LD::st(lA[2][q], posA + 2 * LWP, v);
+        LD::st(lA[0][q], pos_x(a), v);
+        if (mA0 == mfirst) LD::st(lA[2][q], pos_x(a), v);
       }
-      if (mA0 + 1 <= mlast && mA0 < ke) dma(a, mA0 + 1);
+      if (mA0 + 1 <= mlast) dma(a, mA0 + 1);                // consumed in the first step's stage-B slot
     }
     if (mA0 + 1 <= mlast) pair_load<SA>(a, pbo(mA0 + 1), R[1]);
     KA[2][0] = KA[2][1] = zero2;
@@ -1536,19 +1584,6 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
           LD::st(lA[sAp][q], posA, v);
           if (ZREG) IA[sAp][q] = v;
         }
-      }
-      if (is_x(A0)) {
-        // the extra position as this thread's own: plane mm + 1's operands from the staging (its
-        // DMA went out one iteration ago, ahead of that iteration's NLA look-ahead loads: all but
-        // the NLA - 1 youngest vector-memory operations done means it has landed), then plane
-        // mm + 2's DMA ahead of this iteration's look-ahead, after the staging's reads (asm
-        // "memory" clobbers) -- not in the chunk's last step, so that no DMA is left outstanding
-        // when the workgroup ends
-        if (mm + 1 <= mlast) {
-          pair_x_wait<NLA - 1>();
-          xstore(A0, sAp);
-        }
-        if (mm + 2 <= mlast && mm < ke) dma(A0, mm + 2);
       }
       if (mm + 2 <= mlast) pair_load<SA>(A0, pbo(mm + 2), rnn);          // look-ahead
     }
@@ -1690,6 +1725,23 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
           // gl: x(t+h) = x + coef (0.5 (0.0 + 0.0) + 2.0 0.0), stored unless XN already holds it
           if (!GLX && !A2.gl_keep) stb(A2.out + 2 * A2.fs, e0, dbl2{ro.x[2][0] + A2.glX, ro.x[2][1] + A2.glX});
         }
+      }
+    }
+    {
+      PFT_PAIR_BIND(A3, C3);
+      (void)C3;
+      if (is_x(A3)) {
+        // the extra positions, in the last wave's stage-B slot (it holds no stage-B position, its
+        // SIMD has a wave-phase to spare: pair_pos), after stage B, where few registers are live:
+        // plane mm + 1's operands from the staging (its DMA went out an iteration ago; the wait for
+        // everything this wave issued is only the last wave's), stage A's input into lA, then plane
+        // mm + 2's DMA -- not in the chunk's last step, so that no DMA is left outstanding when the
+        // workgroup ends
+        if (mm + 1 <= mlast) {
+          pair_x_wait<0>();
+          xstore(A3, (PH + 1) % 3);
+        }
+        if (mm + 2 <= mlast && mm < ke) dma(A3, mm + 2);
       }
     }
     if (mm == ke) return false;
