@@ -2242,6 +2242,7 @@ struct pft_slab {
   } book[2];
   int kz;                // planes per workgroup z-march; 0 = automatic (z-chunk cost model)
   int n_cu;               // compute units of the slab's device
+  int cu_reserved;        // of them kept off the compute stream for the boundary launches (CU mask)
   double* noise;         // device u_noise (n3*plane) or null
   int tile_wx;           // 32 / 16: LDS-tiled kernels with that many pairs per row; 1: automatic;
                          // 2: LDS-tiled at any size, automatic tile; 0: cache-based
@@ -2779,7 +2780,7 @@ static void kz_memo_put(pft_slab* s, int slot, long key, int kz)
 // The cheapest count wins (more chunks only when 5% cheaper).
 static int chunk_kz(pft_slab* s, int slot, int occ, long ntile, int nplanes)
 {
-  const long key = ((long)occ << 52) ^ (ntile << 24) ^ (long)nplanes;
+  const long key = ((long)occ << 52) ^ ((long)s->cu_reserved << 44) ^ (ntile << 24) ^ (long)nplanes;
   int kz = kz_memo_get(s, slot, key);
   if (kz) return kz;
   int best_nch = 1;
@@ -2788,7 +2789,8 @@ static int chunk_kz(pft_slab* s, int slot, int occ, long ntile, int nplanes)
     const int k = (nplanes + nch - 1) / nch;
     if (nch > 1 && k == (nplanes + nch - 2) / (nch - 1)) continue;   // same kz as nch - 1
     const long nb = ntile * ((nplanes + k - 1) / k);
-    const long per_cu = (nb + s->n_cu - 1) / s->n_cu;
+    const int ncu = s->n_cu - s->cu_reserved;   // the compute stream's CUs (launches on it chunk here)
+    const long per_cu = (nb + ncu - 1) / ncu;
     const double rounds = occ <= 2 ? (double)((per_cu + occ - 1) / occ) : std::max(1.0, (double)per_cu / occ);
     const double cost = rounds * (k + 2);
     if (best_cost < 0.0 || cost < 0.95 * best_cost) { best_cost = cost; best_nch = nch; }
@@ -4129,6 +4131,29 @@ int pft_slab_set_boundary_stream(pft_slab* s, int on)
   const char* eb = getenv("PFT_CE_BND");
   const char* es = getenv("PFT_CE_STREAMS");
   s->bnd_mode = !on ? 0 : eb && atoi(eb) >= 0 && atoi(eb) <= 3 ? atoi(eb) : 3;
+  {
+    // CUs reserved for the boundary launches (PFT_CE_RESERVE=R): the compute stream is re-created
+    // with a CU mask that leaves R CUs out, so an interior launch of several rounds of workgroups
+    // can never hold the CUs the boundary launch beside it needs.  R/8 per XCD, chosen so that
+    // either numbering of the mask (CU-major per XCD or XCD-interleaved) spreads them evenly.
+    const char* er = getenv("PFT_CE_RESERVE");
+    const int want = on && s->bnd_mode >= 2 && er ? atoi(er) : 0;
+    if (want != s->cu_reserved && want >= 0 && want <= 32 && want % 8 == 0 && s->n_cu == 256) {
+      uint32_t mask[8];
+      for (int w = 0; w < 8; ++w) mask[w] = ~0u;
+      for (int x = 0; x < 8; ++x)
+        for (int j = 0; j < want / 8; ++j) {
+          const int bit = 32 * x + 8 * j + x;   // residue x mod 8, in the block of 32 numbered x
+          mask[bit / 32] &= ~(1u << (bit % 32));
+        }
+      hipStream_t ns = nullptr;
+      HIPCHK(hipStreamSynchronize(s->stream));
+      HIPCHK(hipExtStreamCreateWithCUMask(&ns, 8, mask));
+      HIPCHK(hipStreamDestroy(s->stream));
+      s->stream = ns;
+      s->cu_reserved = want;
+    }
+  }
   s->ce_streams = es && atoi(es) == 1 ? 1 : 2;
   if (s->ce_streams == 2 && !s->ev_copy) HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
   if (!s->ev_side) HIPCHK(hipEventCreateWithFlags(&s->ev_side, hipEventDisableTiming));
