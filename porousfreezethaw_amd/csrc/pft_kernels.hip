@@ -1389,7 +1389,7 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   // threads beyond the R2 positions shadow the last one (same loads and LDS writes, no stores)
   const int tt = min((int)threadIdx.x, NPOS - 1);
   int px, py;
-  if (NPOS > PFT_PBLOCK) {
+  if (LWP == 22 && NPOS > PFT_PBLOCK) {
     pair_pos(tt, TX / 2, TY, px, py);
   } else {
     // no extra positions: row-major over the R2 tile, as measured best there (200^3: the stage-B
@@ -1436,7 +1436,8 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
     asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
     return l;
   };
-  auto is_x = [&](const PairArgs& A) { return wid == PFT_PBLOCK / 64 - 1 && lane() >= 64 - nex(A); };
+  // (only tiles wider than 20 cells have them: the 12-pair pitch compiles the extras out)
+  auto is_x = [&](const PairArgs& A) { return LWP == 22 && wid == PFT_PBLOCK / 64 - 1 && lane() >= 64 - nex(A); };
   // the extra position's column (row ty + 3) and its acting pair's offset in a plane
   auto px_x = [&](const PairArgs& A) { return lane() - 64 + (A.tx / 2 + 2); };
   auto apo_x = [&](const PairArgs& A) { return lXa[lane() - (64 - nex(A))]; };
@@ -3561,7 +3562,8 @@ static bool pair_geometry_ok(int tx, int ty)
 {
   const int lwp = pair_lwp(tx);
   // positions: one per thread, and up to PFT_PAIR_NEX more in the last ring row (LDS DMA)
-  return tx >= 2 && tx % 2 == 0 && ty >= 1 && (tx / 2 + 2) * (ty + 4) <= PFT_PBLOCK + PFT_PAIR_NEX &&
+  return tx >= 2 && tx % 2 == 0 && ty >= 1 &&
+         (tx / 2 + 2) * (ty + 4) <= (lwp == 22 ? PFT_PBLOCK + PFT_PAIR_NEX : PFT_PBLOCK) &&
          (tx / 2 + 2) * (ty + 3) <= PFT_PBLOCK && tx / 2 + 2 <= 22 &&
          2 * PFT_PAIR_PADP + lwp * (ty + 4) <= PFT_PAIR_H && 2 * PFT_PAIR_PADP + lwp * (ty + 2) <= PFT_PAIR_HB &&
          (tx / 2) * ty <= PFT_PAIR_OPN;
