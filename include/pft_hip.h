@@ -132,6 +132,14 @@ int pft_slab_stage(pft_slab * s, int stage, double t_stage, double coef, double 
 /* k_begin value selecting planes 0, 1 and n3-2, n3-1 in one launch (what the z-neighbours' pair
    kernels read: the two-plane halo) */
 #define PFT_K_BOUNDARY2 (-3)
+/* pair kernels only: the PFT_K_BOUNDARY2 chunks lead the grid of the interior launch [2, n3-2), one
+   launch; the copy-engine exchange that follows starts when those workgroups are done
+   (pft_slab_boundary_inline) */
+#define PFT_K_INLINE (-4)
+/* pair kernels only: the whole slab in one launch whose first workgroups are the first and the last
+   z-chunk of every tile column (at least three chunks); the copy-engine exchange that follows starts
+   when those are done */
+#define PFT_K_ENDS_FIRST (-5)
 
 /* K = f(input) only (RK_RightHandSide semantics), input/output buffer indices */
 int pft_slab_rhs(pft_slab * s, int in_buf, int out_buf, double t);
@@ -310,6 +318,13 @@ int pft_slab_halo_mark(pft_slab * s);
    the compute stream wait for it before the next launch (its planes are that launch's input).  The
    boundary launch takes the second set of error-norm shards. */
 int pft_slab_set_boundary_stream(pft_slab * s, int on);
+/* the pair kernels' inline boundary: PFT_K_INLINE (the copy-engine exchange's boundary placement 4,
+   PFT_CE_BND=4), PFT_K_ENDS_FIRST (placement 5), or 0 (a separate boundary launch or none) */
+int pft_slab_boundary_inline(const pft_slab * s);
+/* the same for the stage launches (their inline boundary can be turned off: PFT_CE_STAGE_INLINE=0) */
+int pft_slab_stage_inline(const pft_slab * s);
+/* the same for one pair kernel (first = 2: stages 2+3, 4: stages 4+5) */
+int pft_slab_pair_inline(const pft_slab * s, int first);
 /* far ghost plane of buffer `which`, field q: side 0 = two planes below the slab (the neighbour
    below's plane n3' - 1; plane -1 of the field), side 1 = two above (the neighbour above's plane
    2; plane n3 + 2) */

@@ -218,6 +218,11 @@ struct StageArgs {
   int has_below, has_above;
   int k_begin, k_end, kz, ntile, nchunk;
   int kspan;           // planes a chunk processes from its start (kz, or 1 for the boundary planes)
+  // inline boundary (merson_fused; as PairArgs): the first nbw workgroups produce the planes the
+  // exchange sends and count themselves in *bdone; bends 1: the first and last chunk of every tile
+  // column, 0: two-plane chunks at each end; the other nint workgroups run chunks c0 ..
+  int nbw, bends, c0, nint;
+  unsigned long long* bdone;
   double T_top;        // Dirichlet value T_top(t_stage), equation.c:110
   double coef, h;
   double em0, em1, em2;
@@ -762,7 +767,7 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
     gw1 = a.gate[1];
     gw2 = a.gate[2];
   }
-  if (STAGE == 1 && (a.npart > 0 || a.gdev) && (int)blockIdx.x == a.ntile * a.nchunk) {
+  if (STAGE == 1 && (a.npart > 0 || a.gdev) && (int)blockIdx.x == a.nbw + a.nint) {
     // the extra workgroup of a speculative stage 1: the previous launch's error norm, then (gated
     // steps) the decision on the step it ended
     unsigned long long m = 0, f = 0;
@@ -777,8 +782,12 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
     return;
   }
   const int ntx = (a.n1 + TX - 1) / TX;
-  const int lin = xcd_remap(blockIdx.x, a.ntile * a.nchunk);
-  const int tile = lin % a.ntile, chunk = lin / a.ntile;
+  // inline boundary: the leading workgroups (dispatched first) produce the planes the exchange sends
+  const bool bw = (int)blockIdx.x < a.nbw;
+  const int lin = bw ? xcd_remap(blockIdx.x, a.nbw) : xcd_remap(blockIdx.x - a.nbw, a.nint);
+  const int tile = lin % a.ntile, cq = lin / a.ntile;
+  const int chunk = bw ? (a.bends ? (cq ? a.nchunk - 1 : 0) : cq) : a.c0 + cq;
+  const bool bshort = bw && !a.bends;
   const int x0 = (tile % ntx) * TX, y0 = (tile / ntx) * TY;
   // threads beyond the WX x TY tile (256 > WX * TY) shadow the tile's last thread: the same loads
   // and LDS writes (same values to the same slots), no global stores
@@ -787,8 +796,8 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
   const int i0 = x0 + 2 * tx, j = y0 + ty;
   const bool active = (i0 < a.n1) && (j < a.n2) && (int)threadIdx.x < WX * TY;
   const long po = (long)(j < a.n2 ? j : a.n2 - 1) * a.n1 + (i0 < a.n1 ? i0 : a.n1 - 2);
-  const int kb = a.k_begin + chunk * a.kz;
-  const int ke = min(kb + a.kspan, a.k_end);
+  const int kb = bshort ? chunk * (a.n3 - 2) : a.k_begin + chunk * a.kz;
+  const int ke = bshort ? kb + 2 : min(kb + a.kspan, a.k_end);
   const int lo = (ty + 1) * LW + 2 + 2 * tx;
 
   const int t = threadIdx.x;
@@ -1039,6 +1048,16 @@ __global__ __launch_bounds__(PFT_FBLOCK) __attribute__((amdgpu_waves_per_eu(STAG
       else eps_arrive(bm, bnf, a.shards, a.eps_bits, a.nonfinite, a.pub, a.pub_count);
     }
   }
+  if (bw) {
+    // an inline boundary workgroup (as merson_pair's): stores done, L2 written back, counted.  (A
+    // gated launch, which may leave before its stores, never runs inline: run_stage)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      __hip_atomic_fetch_add(a.bdone, 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1112,6 +1131,13 @@ struct PairArgs {
                               // from the two-plane halo (ghost + far ghost planes, pft_slab_far)
   int k_begin, k_end, kz, ntile, nchunk, ntx;
   int kspan;            // planes a chunk runs from its start (kz; 2 for the two-plane boundary launch)
+  // inline boundary (PFT_K_INLINE, PFT_K_ENDS_FIRST): the grid's first nbw workgroups produce the
+  // planes the exchange sends, each adding one to *bdone once they are written back (nbw 0: none).
+  // bends 0: they run the two planes at each end (chunk 0: planes 0, 1; chunk 1: n3 - 2, n3 - 1)
+  // and the other nint workgroups the chunks of [k_begin, k_end); bends 1: one launch of the whole
+  // slab's chunks, the first and the last chunk of every tile column first, then chunks c0 ..
+  int nbw, bends, c0, nint;
+  unsigned long long* bdone;
   int tx, ty;           // R0 tile: tx cells (even) x ty rows
   double T_topA, T_topB;   // Dirichlet u above the top plane at the two stage times
   double cinA, cinB;    // stage-input coefficients: h/3, h/6 (2+3); h/8, h (4+5)
@@ -1383,8 +1409,12 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
   __shared__ unsigned lXa[PFT_PAIR_NEX];
 
   const int TX = a.tx, TY = a.ty, WP2 = TX / 2 + 2, NPOS = WP2 * (TY + 4);
-  const int lin = xcd_remap(blockIdx.x, a.ntile * a.nchunk);
-  const int tile = lin % a.ntile, chunk = lin / a.ntile;
+  // inline boundary: the leading workgroups (dispatched first) are the boundary chunks
+  const bool bw = (int)blockIdx.x < a.nbw;
+  const int lin = bw ? xcd_remap(blockIdx.x, a.nbw) : xcd_remap(blockIdx.x - a.nbw, a.nint);
+  const int tile = lin % a.ntile, cq = lin / a.ntile;
+  const int chunk = bw ? (a.bends ? (cq ? a.nchunk - 1 : 0) : cq) : a.c0 + cq;
+  const bool bshort = bw && !a.bends;   // a two-plane boundary chunk (PFT_K_INLINE)
   const int x0 = (tile % a.ntx) * TX, y0 = (tile / a.ntx) * TY;
   // threads beyond the R2 positions shadow the last one (same loads and LDS writes, no stores)
   const int tt = min((int)threadIdx.x, NPOS - 1);
@@ -1475,8 +1505,8 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
     }
   };
 
-  const int kb = a.k_begin + chunk * a.kz;
-  const int ke = min(kb + a.kspan, a.k_end);
+  const int kb = bshort ? chunk * (a.n3 - 2) : a.k_begin + chunk * a.kz;
+  const int ke = bshort ? kb + 2 : min(kb + a.kspan, a.k_end);
   const int n3 = a.n3;
   const bool wlo = !a.has_below, whi = !a.has_above;         // walls (equation.c:164-183)
   // stage-A planes [mA0, mA1]: the chunk's planes and one on each side -- at a slab interface
@@ -1787,8 +1817,29 @@ __global__ __launch_bounds__(PFT_PBLOCK) __attribute__((amdgpu_waves_per_eu(2)))
       else eps_arrive(bm, bnf, a.shards, a.eps_bits, a.nonfinite, a.pub, a.pub_count);
     }
   }
+  if (bw) {
+    // an inline boundary workgroup: every wave's stores done, then one lane writes the XCD's L2
+    // back (system scope: the copy engines read memory, not this L2) and counts the workgroup; the
+    // copies wait for the count (bnd_trigger_kernel) while the interior workgroups go on
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      __hip_atomic_fetch_add(a.bdone, 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 #pragma clang diagnostic pop
+
+// the copy-engine exchange of an inline boundary (PFT_K_INLINE): this one-wave kernel ends once the
+// boundary workgroups of the launch have counted themselves (*bdone >= target, monotonic), so the
+// plane copies queued behind it on the comm stream start while that launch's interior still runs.
+// It sits on a CU the boundary workgroups freed; nothing it waits for depends on another rank.
+__global__ __launch_bounds__(64) void bnd_trigger_kernel(const unsigned long long* bdone, unsigned long long target)
+{
+  if (threadIdx.x == 0)
+    while (__hip_atomic_load(bdone, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(2);
+}
 
 // ------------------------------------------------------------------------------------------
 // f1: the default Params' initial condition and the glass beads on the device (pft_slab_ic_default)
@@ -2181,6 +2232,15 @@ struct pft_slab {
   int wait_streamops;    // A/B: halo waits as hipStreamWaitValue64 (env PFT_WAIT_STREAMOPS=1)
   hipStream_t bnd;
   hipEvent_t ev_bnd, ev_pre, ev_copy, ev_side, ev_join;
+  // bnd_mode 4 (inline boundary): the pair kernels' boundary chunks lead their interior launch
+  // (PFT_K_INLINE); its boundary workgroups count themselves in *bdone, and the exchange's copies
+  // wait behind bnd_trigger_kernel for the count bdone_target (inline_pending: not yet sent)
+  unsigned long long* bdone;
+  unsigned long long bdone_target;
+  int inline_pending;
+  int trig_early;        // A/B (PFT_CE_TRIG): 1 the trigger queued with the launch, 0 with the copies
+  int stage_inline;      // A/B (PFT_CE_STAGE_INLINE): stage launches inline too (else boundary first)
+  hipEvent_t ev_trig;
   int put_role, put_f0, put_f1, put_deep;   // the exchange the last halo_put2 sent (its wait receives it)
   SlabPeer peer[2];              // [0] the neighbour below, [1] above
   int drop_puts;                 // fault injection: halo puts and flag raises skipped (PFT_IPC_DROP_PUTS)
@@ -2555,6 +2615,8 @@ int pft_slab_destroy(pft_slab* s)
   if (s->ev_copy) (void)hipEventDestroy(s->ev_copy);
   if (s->ev_side) (void)hipEventDestroy(s->ev_side);
   if (s->ev_join) (void)hipEventDestroy(s->ev_join);
+  if (s->ev_trig) (void)hipEventDestroy(s->ev_trig);
+  if (s->bdone) (void)hipFree(s->bdone);
   for (int i = 0; i < 2; ++i) {
     if (s->ev_seq[i]) (void)hipEventDestroy(s->ev_seq[i]);
     if (s->ev_planes[i]) (void)hipEventDestroy(s->ev_planes[i]);
@@ -2779,16 +2841,19 @@ static void kz_memo_put(pft_slab* s, int slot, long key, int kz)
 //   - occ >= 3: max(1, w / occ) -- retiring workgroups are refilled at once, and the extra
 //     workgroups help the arithmetic-heavy stages hide latency.
 // The cheapest count wins (more chunks only when 5% cheaper).
-static int chunk_kz(pft_slab* s, int slot, int occ, long ntile, int nplanes)
+static int chunk_kz(pft_slab* s, int slot, int occ, long ntile, int nplanes, int min_nch = 1)
 {
   const long key = ((long)occ << 52) ^ ((long)s->cu_reserved << 44) ^ (ntile << 24) ^ (long)nplanes;
   int kz = kz_memo_get(s, slot, key);
   if (kz) return kz;
   int best_nch = 1;
   double best_cost = -1.0;
-  for (int nch = 1; nch <= nplanes; ++nch) {
+  if (min_nch > nplanes) min_nch = nplanes;
+  for (int nch = min_nch; nch <= nplanes; ++nch) {
     const int k = (nplanes + nch - 1) / nch;
-    if (nch > 1 && k == (nplanes + nch - 2) / (nch - 1)) continue;   // same kz as nch - 1
+    if (nch > min_nch && k == (nplanes + nch - 2) / (nch - 1)) continue;   // same kz as nch - 1
+    if ((nplanes + k - 1) / k < min_nch) continue;
+    if (min_nch >= 3 && (k < 2 || nplanes - ((nplanes + k - 1) / k - 1) * k < 2)) continue;   // edge chunks >= 2 planes
     const long nb = ntile * ((nplanes + k - 1) / k);
     const int ncu = s->n_cu - s->cu_reserved;   // the compute stream's CUs (launches on it chunk here)
     const long per_cu = (nb + ncu - 1) / ncu;
@@ -2796,6 +2861,7 @@ static int chunk_kz(pft_slab* s, int slot, int occ, long ntile, int nplanes)
     const double cost = rounds * (k + 2);
     if (best_cost < 0.0 || cost < 0.95 * best_cost) { best_cost = cost; best_nch = nch; }
   }
+  if (best_cost < 0.0) best_nch = std::max(1, nplanes);
   kz = (nplanes + best_nch - 1) / best_nch;
   kz_memo_put(s, slot, key, kz);
   return kz;
@@ -2883,8 +2949,15 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   // one-plane chunks n3 - 1 planes apart (what the z-neighbours need first)
   const bool bnd = k_begin == PFT_K_BOUNDARY || k_begin == PFT_K_BOUNDARY2;
   const int bdepth = k_begin == PFT_K_BOUNDARY2 ? 2 : 1;   // PFT_K_BOUNDARY2: planes 0, 1 and n3-2, n3-1
-  if (bnd) {
-    k_begin = 0;
+  // inline boundary (merson_fused only, never gated): PFT_K_ENDS_FIRST -- the whole slab, the first
+  // and last chunk of every tile column leading -- or PFT_K_INLINE -- two-plane chunks at each end
+  // leading the interior [2, n3 - 2); ENDS_FIRST falls back to INLINE where the chunks cannot hold
+  // the two planes at each end
+  bool ends = k_begin == PFT_K_ENDS_FIRST;
+  const bool inl = k_begin == PFT_K_INLINE || ends;
+  if (inl && (kind != KFUSED || !s->bdone || s->d.n3 < 5 || s->gate_use_seq)) return -2;
+  if (bnd || inl) {
+    k_begin = 0;   // (inline: the planes are set below, once the chunking is known)
     k_end = s->d.n3;
   }
   if (k_begin < 0) k_begin = 0;
@@ -2932,9 +3005,24 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
   } else {
     a.ntile = (s->plane + PFT_BLOCK - 1) / PFT_BLOCK;
   }
+  if (ends) {
+    const int n3 = s->d.n3;
+    const int occ = stage_occupancy(stage, mode, gls, kind, wx);
+    const int kz = s->kz > 0 ? s->kz : chunk_kz(s, 14, occ, a.ntile, n3, 3);
+    const int nch = (n3 + kz - 1) / kz;
+    if (kz < 2 || nch < 3 || n3 - (nch - 1) * kz < 2) ends = false;
+  }
+  if (inl) {
+    k_begin = ends ? 0 : 2;
+    k_end = ends ? s->d.n3 : s->d.n3 - 2;
+    a.k_begin = k_begin;
+    a.k_end = k_end;
+  }
   const int nplanes = k_end - k_begin;
   if (s->kz > 0) {
     a.kz = s->kz;
+  } else if (ends) {
+    a.kz = chunk_kz(s, 14, stage_occupancy(stage, mode, gls, kind, wx), a.ntile, nplanes, 3);
   } else {
     // automatic (chunk_kz)
     // Measured at 400^3 (80 tiles):
@@ -2951,6 +3039,19 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
     a.kz = std::max(1, s->d.n3 - bdepth);
     a.kspan = bdepth;
     a.nchunk = s->d.n3 > bdepth ? 2 : 1;
+  }
+  a.nint = a.ntile * a.nchunk;
+  if (inl) {
+    a.bdone = s->bdone;
+    if (ends) {
+      const int nb = std::min(a.nchunk, 2);
+      a.nbw = nb * a.ntile;
+      a.bends = 1;
+      a.c0 = 1;
+      a.nint = (a.nchunk - nb) * a.ntile;
+    } else {
+      a.nbw = 2 * a.ntile;
+    }
   }
   a.T_top = t_stage < s->c.phase_switch_time ? s->c.top_temp1 : s->c.top_temp2;
   a.coef = coef;
@@ -2985,7 +3086,7 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
     s->pub_armed = 1;
     s->pub_slot = j;
   }
-  dim3 g((unsigned)(a.ntile * a.nchunk));
+  dim3 g((unsigned)(a.nbw + a.nint));
   bool extra = false;
   // a stage launch's interior fills the chip: its boundary runs beside it only in bnd_mode 1 (slower:
   // the two launches' workgroups are dealt interleaved and the interior ends late).  In the boundary
@@ -3040,6 +3141,15 @@ static int run_stage(pft_slab* s, int stage, const double* in, double* kout, dou
     s->bnd_pending = 1;
   } else if (bnd) {
     s->bnd_split = 1;   // a boundary launch before its interior on the compute stream
+  }
+  if (inl) {
+    // as run_pair: the copies' trigger queued with the launch
+    s->bdone_target += (unsigned long long)a.nbw;
+    s->inline_pending = 1;
+    if (s->trig_early) {
+      bnd_trigger_kernel<<<1, 64, 0, s->comm>>>(s->bdone, s->bdone_target);
+      HIPCHK(hipGetLastError());
+    }
   }
   return 0;
 }
@@ -3644,9 +3754,26 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
   a.plane = s->plane;
   a.has_below = s->d.has_below;
   a.has_above = s->d.has_above;
-  // k_begin == PFT_K_BOUNDARY2: planes 0, 1 and n3-2, n3-1 in one launch (two 2-plane chunks)
+  // k_begin == PFT_K_BOUNDARY2: planes 0, 1 and n3-2, n3-1 in one launch (two 2-plane chunks);
+  // PFT_K_INLINE: those chunks first, then the interior [2, n3 - 2), in one launch (bnd_mode 4)
   const bool bnd = k_begin == PFT_K_BOUNDARY2;
+  bool ends = k_begin == PFT_K_ENDS_FIRST;
+  const bool inl = k_begin == PFT_K_INLINE || ends;
+  if (ends) {
+    // the first and the last chunk must hold the two planes at each end (kz >= 2, a last chunk of
+    // two planes or more) and leave a chunk between them; otherwise the two-plane boundary chunks
+    const int n3 = s->d.n3;
+    const int occ = first == 2 ? pair_occupancy_mode<2, false>(mode) : pair_occupancy_mode<4, false>(mode);
+    const int kz = s->kz > 0 ? s->kz : chunk_kz(s, 14 + (first == 4 ? 1 : 0), occ, s->pair_ntile, n3, 3);
+    const int nch = (n3 + kz - 1) / kz;
+    if (kz < 2 || nch < 3 || n3 - (nch - 1) * kz < 2) ends = false;
+  }
+  if (inl && (!s->bdone || s->d.n3 < 5)) return -2;
   a.shards = s->eps_shards + (bnd ? PFT_EPS_SHARDS : 0);
+  if (inl) {
+    k_begin = ends ? 0 : 2;
+    k_end = ends ? s->d.n3 : s->d.n3 - 2;
+  }
   if (bnd || k_begin < 0) k_begin = 0;
   if (bnd || k_end < 0 || k_end > s->d.n3) k_end = s->d.n3;
   if (k_end <= k_begin) return 0;
@@ -3664,15 +3791,32 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
     // z-chunks as run_stage's cost model: a chunk of kz planes evaluates stage A on kz + 2 and
     // loads kz + 3; `occ` workgroups per CU (one: 141 KiB of LDS)
     const int occ = first == 2 ? pair_occupancy_mode<2, false>(mode) : pair_occupancy_mode<4, false>(mode);
-    a.kz = chunk_kz(s, 12 + (first == 4 ? 1 : 0), occ, a.ntile, nplanes);
+    // end chunks first: at least three chunks, so that the first and last of a column are done
+    // while the others still run (the exchange's copies go beside them)
+    a.kz = chunk_kz(s, (ends ? 14 : 12) + (first == 4 ? 1 : 0), occ, a.ntile, nplanes, ends ? 3 : 1);
   }
   a.nchunk = (nplanes + a.kz - 1) / a.kz;
   a.kspan = a.kz;
+  a.nint = a.ntile * a.nchunk;
   if (bnd) {
     a.kz = std::max(1, s->d.n3 - 2);
     a.kspan = 2;
     a.nchunk = s->d.n3 > 2 ? 2 : 1;
+    a.nint = a.ntile * a.nchunk;
   }
+  if (inl) {
+    a.bdone = s->bdone;
+    if (ends) {
+      const int nb = std::min(a.nchunk, 2);
+      a.nbw = nb * a.ntile;
+      a.bends = 1;
+      a.c0 = 1;
+      a.nint = (a.nchunk - nb) * a.ntile;
+    } else {
+      a.nbw = 2 * a.ntile;
+    }
+  }
+  const long nwg = (long)a.nbw + (long)a.nint;   // the launch's workgroups
   a.T_topA = t_a < s->c.phase_switch_time ? s->c.top_temp1 : s->c.top_temp2;
   a.T_topB = t_b < s->c.phase_switch_time ? s->c.top_temp1 : s->c.top_temp2;
   // exactly the solver's h/3.0, h/6.0 and h/8.0 (and run_stage's stage-input coefficients)
@@ -3690,11 +3834,11 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
   s->pub_armed = 0;
   const int split_pub = s->split_pub;
   s->split_pub = 0;
-  if (first == 4 && s->inkernel_pub && !bnd && k_begin == 0 && k_end == s->d.n3) {
+  if (first == 4 && s->inkernel_pub && !bnd && ((k_begin == 0 && k_end == s->d.n3) || inl)) {
     const int j = (int)(s->pub_next % PFT_PUB_SLOTS);
     __atomic_store_n(&s->pub_ring[2 * j], PFT_PUB_SENTINEL, __ATOMIC_RELEASE);
     __atomic_store_n(&s->pub_ring[2 * j + 1], PFT_PUB_SENTINEL, __ATOMIC_RELEASE);
-    const int rc = defer_arm(s, (long)a.ntile * a.nchunk, j, &a.part);
+    const int rc = defer_arm(s, nwg, j, &a.part);
     if (rc) return rc;
     s->pub_armed = 1;
     s->pub_slot = j;
@@ -3715,7 +3859,7 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
     s->pub_armed = 1;
     s->pub_slot = s->defer_slot;
   }
-  const dim3 g((unsigned)(a.ntile * a.nchunk));
+  const dim3 g((unsigned)nwg);
   hipStream_t st = s->stream;
   // bnd_mode 1, 2: the boundary launch beside the interior one.  On a 400 x 400 plane the interior
   // holds one workgroup per tile column, 220 of 256 CUs: the boundary's workgroups take the CUs it
@@ -3740,6 +3884,18 @@ static int run_pair(pft_slab* s, int first, double t_a, double t_b, double h, do
   if (beside) {
     HIPCHK(hipEventRecord(s->ev_bnd, s->bnd));
     s->bnd_pending = 1;
+  }
+  if (inl) {
+    s->bdone_target += (unsigned long long)a.nbw;
+    s->inline_pending = 1;
+    // the copies' trigger, on the comm stream at once: queued now, it is normally dispatched while
+    // the previous launch still runs and sits on its CU before this launch fills the chip (pair 4+5
+    // at 256 VGPRs leaves no room beside its workgroups: a trigger queued later waited for a CU
+    // until this launch drained -- the copies then ran after it)
+    if (s->trig_early) {
+      bnd_trigger_kernel<<<1, 64, 0, s->comm>>>(s->bdone, s->bdone_target);
+      HIPCHK(hipGetLastError());
+    }
   }
   return 0;
 }
@@ -3780,6 +3936,26 @@ int pft_slab_pair_geometry(const pft_slab* s, int* tx, int* ty)
 int pft_slab_pair(pft_slab* s, int first, double t_a, double t_b, double h, double coef)
 {
   return pft_slab_pair_range(s, first, t_a, t_b, h, coef, -1, -1);
+}
+
+int pft_slab_boundary_inline(const pft_slab* s)
+{
+  return s->bnd_mode >= 4 && s->bdone && s->d.n3 >= 5 && slab_kind(s) == KFUSED
+             ? (s->bnd_mode == 5 ? PFT_K_ENDS_FIRST : PFT_K_INLINE)
+             : 0;
+}
+
+int pft_slab_stage_inline(const pft_slab* s) { return s->stage_inline ? pft_slab_boundary_inline(s) : 0; }
+
+int pft_slab_pair_inline(const pft_slab* s, int first)
+{
+  const int m = pft_slab_boundary_inline(s);
+  if (!m) return 0;
+  // A/B: PFT_CE_BND23 / PFT_CE_BND45 = 4 or 5 overrides the placement of one pair kernel
+  const char* e = getenv(first == 2 ? "PFT_CE_BND23" : "PFT_CE_BND45");
+  if (e && atoi(e) == 4) return PFT_K_INLINE;
+  if (e && atoi(e) == 5) return PFT_K_ENDS_FIRST;
+  return m;
 }
 
 int pft_slab_pair_range(pft_slab* s, int first, double t_a, double t_b, double h, double coef, int k_begin,
@@ -4037,10 +4213,25 @@ int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsign
   // flag.  (Four streams, a side's copies alternating between two, measured slower: 11 300-12 600
   // against 16 000 Mcells*steps/s on the 800^3 rank slab, profiles/r05_ce_ab.txt; removed.)
   hipStream_t cs[2] = {s->comm, s->ce_streams == 1 ? s->comm : s->side};
-  hipEvent_t ready = s->bnd_pending ? s->ev_bnd : s->ev_order[0];
-  if (!s->bnd_pending && !marked) HIPCHK(hipEventRecord(s->ev_order[0], s->stream));
-  HIPCHK(hipStreamWaitEvent(cs[0], ready, 0));
-  if (cs[1] != cs[0]) HIPCHK(hipStreamWaitEvent(cs[1], ready, 0));
+  if (s->inline_pending) {
+    // inline boundary: the copies start once the launch's boundary workgroups have counted
+    // themselves -- not at its end, and with no event on the compute stream between them
+    // (trig_early: the trigger is on the comm stream already, queued with the launch)
+    s->inline_pending = 0;
+    if (!s->trig_early) {
+      bnd_trigger_kernel<<<1, 64, 0, cs[0]>>>(s->bdone, s->bdone_target);
+      HIPCHK(hipGetLastError());
+    }
+    if (cs[1] != cs[0]) {
+      HIPCHK(hipEventRecord(s->ev_trig, cs[0]));
+      HIPCHK(hipStreamWaitEvent(cs[1], s->ev_trig, 0));
+    }
+  } else {
+    hipEvent_t ready = s->bnd_pending ? s->ev_bnd : s->ev_order[0];
+    if (!s->bnd_pending && !marked) HIPCHK(hipEventRecord(s->ev_order[0], s->stream));
+    HIPCHK(hipStreamWaitEvent(cs[0], ready, 0));
+    if (cs[1] != cs[0]) HIPCHK(hipStreamWaitEvent(cs[1], ready, 0));
+  }
   const int ph = s->phys[role];
   const long P = s->plane, n3 = s->d.n3;
   const long slot = (long)(seq & 1) * 12 * P;
@@ -4104,7 +4295,7 @@ int pft_slab_halo_put_ce(pft_slab* s, int role, int f0, int f1, int deep, unsign
 int pft_slab_halo_mark(pft_slab* s)
 {
   if (s->ipc_poisoned) return slab_poisoned(s, "pft_slab_halo_mark");
-  if (!s->bnd_pending) HIPCHK(hipEventRecord(s->ev_order[0], s->stream));
+  if (!s->bnd_pending && !s->inline_pending) HIPCHK(hipEventRecord(s->ev_order[0], s->stream));
   s->ce_marked = 1;
   return 0;
 }
@@ -4132,7 +4323,21 @@ int pft_slab_set_boundary_stream(pft_slab* s, int on)
   // on the comm stream (slower)
   const char* eb = getenv("PFT_CE_BND");
   const char* es = getenv("PFT_CE_STREAMS");
-  s->bnd_mode = !on ? 0 : eb && atoi(eb) >= 0 && atoi(eb) <= 3 ? atoi(eb) : 3;
+  s->bnd_mode = !on ? 0 : eb && atoi(eb) >= 0 && atoi(eb) <= 5 ? atoi(eb) : 3;
+  if (s->bnd_mode >= 4 && !s->bdone) {
+    HIPCHK(hipMalloc((void**)&s->bdone, 64));
+    HIPCHK(hipMemsetAsync(s->bdone, 0, 64, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    s->bdone_target = 0;
+    HIPCHK(hipEventCreateWithFlags(&s->ev_trig, hipEventDisableTiming));
+  }
+  s->inline_pending = 0;
+  {
+    const char* et = getenv("PFT_CE_TRIG");
+    const char* esi = getenv("PFT_CE_STAGE_INLINE");
+    s->trig_early = et ? atoi(et) != 0 : 1;
+    s->stage_inline = esi ? atoi(esi) != 0 : 1;
+  }
   {
     // CUs reserved for the boundary launches (PFT_CE_RESERVE=R): the compute stream is re-created
     // with a CU mask that leaves R CUs out, so an interior launch of several rounds of workgroups

@@ -270,6 +270,14 @@ static int do_stage(int stage, double ts, double coef, double h, long * launches
 		   end first, their exchange on the comm stream beside the interior launch; ipc with put
 		   kernels: the whole slab, then the put. */
 		n3 = R.slab_grid.n3;
+		if(pft_comm_boundary_first(c) && n3 >= 5 && (rc = pft_slab_stage_inline(R.slab))) {
+			/* one launch whose leading workgroups produce the planes the exchange sends (as do_pair) */
+			if((rc = run1(stage, ts, coef, h, rc, 0))) return rc;
+			if((rc = pft_comm_halo_start_deep(c, out_buf, 0, nfields))) return rc;
+			if(R.tstep) pft_slab_timing_mark(R.slab, tstage, 1);
+			(*launches)++;
+			return pft_comm_halo_finish(c);
+		}
 		if(pft_comm_boundary_first(c) && n3 >= 5) {
 			if((rc = run1(stage, ts, coef, h, PFT_K_BOUNDARY2, 0))) return rc;
 			if((rc = pft_comm_halo_start_deep(c, out_buf, 0, nfields))) return rc;
@@ -324,6 +332,16 @@ static int do_pair(int first, double ta, double tb, double h, double coef, long 
 		   exchange (K3, or x(t+h): gl only where stored) beside the interior launch, which reads no
 		   ghost plane */
 		const int nf = pft_slab_stage_fields(R.slab, first+1);
+		const int inl = pft_slab_pair_inline(R.slab, first);
+		if(inl) {
+			/* one launch whose leading workgroups produce the planes the exchange sends; the copies
+			   start when they are done (PFT_K_INLINE, PFT_K_ENDS_FIRST) */
+			(*launches)++;
+			if((rc = pft_slab_pair_range(R.slab, first, ta, tb, h, coef, inl, 0))) return rc;
+			if((rc = pft_comm_halo_start_deep(c, out_buf, 0, nf))) return rc;
+			if(R.tstep) pft_slab_timing_mark(R.slab, first+1, 1);
+			return pft_comm_halo_finish(c);
+		}
 		*launches += 2;
 		if((rc = pft_slab_pair_range(R.slab, first, ta, tb, h, coef, PFT_K_BOUNDARY2, 0))) return rc;
 		if((rc = pft_comm_halo_start_deep(c, out_buf, 0, nf))) return rc;

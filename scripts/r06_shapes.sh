@@ -18,6 +18,8 @@ for rep in $(seq ${REPS:-2}); do
         ipc) timeout -k 10 300 python bench.py $args --self-exchange --transport ipc > $f 2>>$OUT/err.log ;;
         ce) timeout -k 10 300 python bench.py $args --self-exchange --transport ipc-ce > $f 2>>$OUT/err.log ;;
         ce0) PFT_CE_BND=0 timeout -k 10 300 python bench.py $args --self-exchange --transport ipc-ce > $f 2>>$OUT/err.log ;;
+        ce4) PFT_CE_BND=4 timeout -k 10 300 python bench.py $args --self-exchange --transport ipc-ce > $f 2>>$OUT/err.log ;;
+        ce5) PFT_CE_BND=5 timeout -k 10 300 python bench.py $args --self-exchange --transport ipc-ce > $f 2>>$OUT/err.log ;;
       esac
       rc=$?; [ $rc -ne 0 ] && { echo "$name $v failed: $rc"; exit $rc; }
       python3 -c "import json;d=json.load(open('$f'));print('$name $v rep $rep'.ljust(20), d['value'], d['ms_per_step'], (d['roofline'] or {}).get('stages_ms'), d['config'].get('pair_tile'))"

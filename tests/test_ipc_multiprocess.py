@@ -212,8 +212,12 @@ def test_lost_ipc_halo_ends_in_device_error_not_a_hang(tmp_path):
 # copy-engine options (pft_slab_set_boundary_stream): by default the boundary pipeline (PFT_CE_BND 3:
 # the pair kernels' boundary launch beside their interior launch, the halo waits on the boundary
 # stream, so no pair interior launch waits for a neighbour); 2: the same with the waits on the
-# compute stream; 0: every boundary launch before its interior; 1: every one beside
+# compute stream; 0: every boundary launch before its interior; 1: every one beside; 4: the pair
+# kernels' boundary chunks inline, leading their interior launch's grid (PFT_K_INLINE); 5: the whole
+# slab in one pair launch, every tile column's first and last z-chunk leading (PFT_K_ENDS_FIRST)
 _SERIAL = {"PFT_CE_BND": "0"}
+_INLINE = {"PFT_CE_BND": "4"}
+_ENDS = {"PFT_CE_BND": "5"}
 _PIPE = {"PFT_CE_BND": "2"}
 _BESIDE_ALL = {"PFT_CE_BND": "1"}
 
@@ -230,7 +234,14 @@ _BESIDE_ALL = {"PFT_CE_BND": "1"}
                                                               (2, 2, 0, (0, 1), dict(_PIPE, PFT_CE_SEQTAB="3")),
                                                               (3, 2, 1, (0, 1, 2), {"PFT_CE_FENCE": "0"}),
                                                               (2, 2, 0, (0, 1), {"PFT_CE_FENCE": "0"}),
-                                                              (3, 2, 0, (0, 2), {"PFT_CE_SEQTAB": "3"})])
+                                                              (3, 2, 0, (0, 2), {"PFT_CE_SEQTAB": "3"}),
+                                                              (2, 2, 0, (0, 1), _INLINE), (3, 2, 1, (0, 1, 2), _INLINE),
+                                                              (3, 2, 0, (1,), _INLINE), (3, 2, 1, (0, 2), _INLINE),
+                                                              (2, 2, 1, (0, 1), dict(_INLINE, PFT_CE_SEQTAB="3")),
+                                                              (2, 2, 0, (0, 1), _ENDS), (3, 2, 1, (0, 1, 2), _ENDS),
+                                                              (3, 2, 0, (1,), _ENDS), (3, 2, 1, (0, 2), _ENDS),
+                                                              (3, 0, 0, (0, 1, 2), _ENDS),
+                                                              (2, 2, 1, (0, 1), dict(_ENDS, PFT_CE_SEQTAB="3"))])
 def test_g20_processes_copy_engine_equal_reference(tmp_path, nranks, pair, staged, ce_ranks, xenv):
     """the boundary planes first, their exchange as SDMA copies and 8-byte flag copies on the comm
     stream beside the interior launch, the receiver's flag wait before the next launch: golden g20
@@ -259,7 +270,8 @@ def test_g20_processes_copy_engine_equal_reference(tmp_path, nranks, pair, stage
         assert np.array_equal(full, A[f"traj_m0_state{i}"])
 
 
-@pytest.mark.parametrize("staged,xenv", [(0, {}), (1, {}), (0, _SERIAL), (1, _SERIAL), (0, _PIPE), (1, _PIPE)])
+@pytest.mark.parametrize("staged,xenv", [(0, {}), (1, {}), (0, _SERIAL), (1, _SERIAL), (0, _PIPE), (1, _PIPE),
+                                         (0, _INLINE), (1, _INLINE), (0, _ENDS), (1, _ENDS)])
 def test_400_processes_copy_engine_equal_one_slab(tmp_path, staged, xenv):
     """400^3 over 2 processes with the pair kernels, the exchange on the copy engines"""
     steps = 10
@@ -279,7 +291,7 @@ def test_400_processes_copy_engine_equal_one_slab(tmp_path, staged, xenv):
     assert np.array_equal(np.concatenate([r["states"][0] for r in res], axis=1), x)
 
 
-@pytest.mark.parametrize("xenv", [{}, _SERIAL, _BESIDE_ALL, _PIPE])
+@pytest.mark.parametrize("xenv", [{}, _SERIAL, _BESIDE_ALL, _PIPE, _INLINE, _ENDS])
 @pytest.mark.parametrize("staged", [0, 1])
 @pytest.mark.parametrize("pair", [2, 0])
 def test_ipc_copy_engine_self_exchange_equals_reference(pair, staged, xenv, monkeypatch):
