@@ -3955,6 +3955,15 @@ int pft_slab_pair_inline(const pft_slab* s, int first)
   const char* e = getenv(first == 2 ? "PFT_CE_BND23" : "PFT_CE_BND45");
   if (e && atoi(e) == 4) return PFT_K_INLINE;
   if (e && atoi(e) == 5) return PFT_K_ENDS_FIRST;
+  // placement 5: end chunks first where the one-wave trigger kernel fits on a CU beside the pair
+  // kernel's workgroup (pair 2+3: 216-221 VGPRs, 126 KiB of LDS).  Pair 4+5 at 256 VGPRs (every
+  // calc mode but 2, scripts/kernel_resources.py) fills each SIMD's register file, so the trigger
+  // holds a CU of its own for as long as it waits -- half the launch with end chunks, and one CU
+  // fewer in one XCD costs that XCD a round of workgroups (400 x 400 x 100: 125 per XCD, 4 rounds
+  // on 32 CUs, 5 on 31; pair 4+5 0.479 against 0.404 ms, profiles/r06_ce_inline.txt).  There the
+  // two-plane boundary chunks (placement 4) free CUs within a few plane steps and the trigger ends
+  // with them.
+  if (m == PFT_K_ENDS_FIRST && first == 4 && s->d.calc_mode != 2) return PFT_K_INLINE;
   return m;
 }
 
@@ -4312,18 +4321,26 @@ int pft_slab_set_boundary_stream(pft_slab* s, int on)
   }
   if (on && !s->ev_copy) HIPCHK(hipEventCreateWithFlags(&s->ev_copy, hipEventDisableTiming));
   // bnd_mode 2: the pair kernels' boundary launch on its own stream beside their interior launch
-  // (run_pair); a stage launch's boundary runs before its interior.  3 (default): the boundary
-  // pipeline -- as 2, and the halo waits on the boundary stream (pft_slab_halo_wait), so that no
-  // pair interior launch waits for a neighbour's flag: a late copy delays only the next boundary
-  // launch, which has the interior's length of slack (profiles/r05_ce_shapes.txt: +1% over 2 on
-  // one GPU).  Env overrides for A/B (profiles/r05_ce_ab.txt, r05_ce_shapes.txt): PFT_CE_BND=2 the
+  // (run_pair); a stage launch's boundary runs before its interior.  3 (round 5's default): the
+  // boundary pipeline -- as 2, and the halo waits on the boundary stream (pft_slab_halo_wait), so
+  // that no pair interior launch waits for a neighbour's flag (profiles/r05_ce_shapes.txt: +1% over 2
+  // on one GPU).  5 (default since round 6): one pair launch per exchange, no boundary launch --
+  // pair 2+3 with every tile column's first and last z-chunk leading the grid (PFT_K_ENDS_FIRST),
+  // pair 4+5 with two-plane boundary chunks leading its interior chunks (PFT_K_INLINE, see
+  // pft_slab_pair_inline); the copies start behind bnd_trigger_kernel once those workgroups are
+  // done, while the rest of the launch runs.  The interior launch of 2 / 3 holds the CUs for
+  // several rounds of workgroups on the driver's N > 1 slabs, so their boundary launch beside it
+  // ran late and its copies after it (profiles/r06_ce_shapes.txt).  4: placement 4 for both pairs.
+  // Stage launches keep their boundary first (inline with PFT_CE_STAGE_INLINE=1: slower, the
+  // boundary workgroups' write-backs in a 3-workgroups-per-CU launch).  Env overrides for A/B
+  // (profiles/r05_ce_ab.txt, r05_ce_shapes.txt, r06_ce_shapes.txt): PFT_CE_BND=2 the
   // waits on the compute stream, 0 every boundary before its interior, 1 every one beside (slower:
   // a stage launch's interior fills the chip, the two launches' workgroups are dealt interleaved
   // and the boundary ends late, profiles/r05_ce_trace_bnd.txt); PFT_CE_STREAMS=1 puts every copy
   // on the comm stream (slower)
   const char* eb = getenv("PFT_CE_BND");
   const char* es = getenv("PFT_CE_STREAMS");
-  s->bnd_mode = !on ? 0 : eb && atoi(eb) >= 0 && atoi(eb) <= 5 ? atoi(eb) : 3;
+  s->bnd_mode = !on ? 0 : eb && atoi(eb) >= 0 && atoi(eb) <= 5 ? atoi(eb) : 5;
   if (s->bnd_mode >= 4 && !s->bdone) {
     HIPCHK(hipMalloc((void**)&s->bdone, 64));
     HIPCHK(hipMemsetAsync(s->bdone, 0, 64, s->stream));
@@ -4336,7 +4353,7 @@ int pft_slab_set_boundary_stream(pft_slab* s, int on)
     const char* et = getenv("PFT_CE_TRIG");
     const char* esi = getenv("PFT_CE_STAGE_INLINE");
     s->trig_early = et ? atoi(et) != 0 : 1;
-    s->stage_inline = esi ? atoi(esi) != 0 : 1;
+    s->stage_inline = esi ? atoi(esi) != 0 : 0;
   }
   {
     // CUs reserved for the boundary launches (PFT_CE_RESERVE=R): the compute stream is re-created

@@ -209,12 +209,13 @@ def test_lost_ipc_halo_ends_in_device_error_not_a_hang(tmp_path):
 
 # ---- the exchange on the copy engines (PFT_IPC_CE=1: pft_slab_halo_put_ce) --------------------
 
-# copy-engine options (pft_slab_set_boundary_stream): by default the boundary pipeline (PFT_CE_BND 3:
-# the pair kernels' boundary launch beside their interior launch, the halo waits on the boundary
+# copy-engine options (pft_slab_set_boundary_stream): PFT_CE_BND 3, round 5's boundary pipeline (the
+# pair kernels' boundary launch beside their interior launch, the halo waits on the boundary
 # stream, so no pair interior launch waits for a neighbour); 2: the same with the waits on the
 # compute stream; 0: every boundary launch before its interior; 1: every one beside; 4: the pair
-# kernels' boundary chunks inline, leading their interior launch's grid (PFT_K_INLINE); 5: the whole
-# slab in one pair launch, every tile column's first and last z-chunk leading (PFT_K_ENDS_FIRST)
+# kernels' boundary chunks inline, leading their interior launch's grid (PFT_K_INLINE); 5 (the
+# default since round 6): pair 2+3 as the whole slab in one launch, every tile column's first and
+# last z-chunk leading (PFT_K_ENDS_FIRST), pair 4+5 as 4 (PFT_CE_BND45=5: ends-first too)
 _SERIAL = {"PFT_CE_BND": "0"}
 _INLINE = {"PFT_CE_BND": "4"}
 _ENDS = {"PFT_CE_BND": "5"}
@@ -241,7 +242,11 @@ _BESIDE_ALL = {"PFT_CE_BND": "1"}
                                                               (2, 2, 0, (0, 1), _ENDS), (3, 2, 1, (0, 1, 2), _ENDS),
                                                               (3, 2, 0, (1,), _ENDS), (3, 2, 1, (0, 2), _ENDS),
                                                               (3, 0, 0, (0, 1, 2), _ENDS),
-                                                              (2, 2, 1, (0, 1), dict(_ENDS, PFT_CE_SEQTAB="3"))])
+                                                              (2, 2, 1, (0, 1), dict(_ENDS, PFT_CE_SEQTAB="3")),
+                                                              (3, 2, 1, (0, 1, 2), dict(_ENDS, PFT_CE_BND45="5")),
+                                                              (3, 2, 0, (0, 1, 2), dict(_ENDS, PFT_CE_STAGE_INLINE="1")),
+                                                              (2, 0, 1, (0, 1), dict(_INLINE, PFT_CE_STAGE_INLINE="1")),
+                                                              (3, 2, 1, (0, 1, 2), {"PFT_CE_BND": "3"})])
 def test_g20_processes_copy_engine_equal_reference(tmp_path, nranks, pair, staged, ce_ranks, xenv):
     """the boundary planes first, their exchange as SDMA copies and 8-byte flag copies on the comm
     stream beside the interior launch, the receiver's flag wait before the next launch: golden g20
