@@ -18,7 +18,7 @@ fatal() { local rc=$1; echo "[$2] exit $rc" | tee -a $O/status.log
 # workloads; unset: both (a gpurun call is limited to 20 minutes)
 PART=${PART:-all}
 if [ "$PART" != 2 ] && [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $O/pytest_gpu.log 2>&1; fatal $? pytest
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 150 --timeout-method thread > $O/pytest_gpu.log 2>&1; fatal $? pytest
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1; fatal $? smoke
 fi
 if [ "$PART" != 2 ]; then
