@@ -562,6 +562,11 @@ def supervise(a):
     world = world_env if launched else a.gpus
     rank = int(os.environ.get("RANK", "0")) if launched else 0
     local = int(os.environ.get("LOCAL_RANK", str(rank))) if launched else 0
+    # stdout carries the one JSON line and nothing else: everything else written to fd 1 from here
+    # on (the gloo library's connection notes under torch.distributed.run) goes to stderr
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     dist = None
     if launched:
         import torch.distributed as dist      # gloo: host only, the supervisors' own rendezvous
@@ -634,8 +639,8 @@ def supervise(a):
                      else "self-spawn (one supervisor, N child ranks)", "attempts": attempts}
     if strong is not None:
         out.setdefault("config", {})["strong"] = strong
-    sys.stdout.write(json.dumps(out) + "\n")
-    sys.stdout.flush()
+    json_out.write(json.dumps(out) + "\n")
+    json_out.flush()
     return 0
 
 

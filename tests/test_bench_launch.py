@@ -82,6 +82,8 @@ def test_torchrun_launch_supervises_one_rank_each():
     assert out["launch"]["mode"].startswith("torchrun")
     assert [a["transport"] for a in out["launch"]["attempts"]] == ["ipc-ce", "rccl"]
     assert sorted(q["rank"] for q in out["config"]["ranks"]) == [0, 1]
+    # stdout is the JSON line alone (the gloo library's connection notes go to stderr)
+    assert json.loads(r.stdout) == out
 
 
 def test_torchrun_launch_propagates_a_rank_failure():
